@@ -1,0 +1,169 @@
+"""Generate the golden fixtures under tests/golden/ -- TEST INFRASTRUCTURE ONLY.
+
+Run in the build container (it reads /root/reference, which does not exist on
+the GPU box):  ``python oracle/gen_golden.py``.
+
+What it pins, and from where:
+
+* ``ref_helpers.npz`` -- outputs of the reference's OWN numpy helpers, imported
+  from /root/reference:
+    - ``tools.params_help.get_neighbour_matrix_by_hand(neighbour_dict_set[0], knn)``
+      for knn = 1..5 (params_help.py:8-20, filter_hub.py:4-24);
+    - ``network.models_att.get_exponential_matrix()`` (models_att.py:14-69),
+      imported with an empty ``tensorflow`` placeholder module because the
+      module does ``import tensorflow as tf`` at top level and TF is not
+      installed (the function itself is pure numpy);
+    - ``tools.data.flip_data / rotate_data / undo`` on seeded inputs
+      (data.py:10-25, 289-322, 269-287), imported with an ``h5py``
+      placeholder (data.py:3 imports it and never uses it).
+* ``notebook_masks.npz`` -- the neighbour matrices printed by the reference's
+  own Kaggle runs (parameter dumps in kaggle/custom-dataset-h36m.ipynb, knn=2,
+  and kaggle/custom-dataset-humansc3d.ipynb, knn=1).
+* ``notebook_facts.json`` -- the learning rates and step arithmetic printed in
+  those logs (lr at step 7798 and 957; total steps 1 559 752 and 95 746).
+* ``oracle_*.npz`` -- float64 oracle forward/gradient/Adam vectors at small
+  sizes (regression pins for the oracle itself; the TF graph arithmetic is
+  unpinned, see oracle/lcn_oracle.py).
+"""
+from __future__ import annotations
+
+import json
+import os
+import re
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+REF = "/root/reference"
+OUT = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, HERE)
+import lcn_oracle as O  # noqa: E402
+
+
+def _import_reference():
+    sys.modules.setdefault("h5py", types.ModuleType("h5py"))
+    sys.modules.setdefault("tensorflow", types.ModuleType("tensorflow"))
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, os.path.join(REF, "tools"))
+    sys.path.insert(0, os.path.join(REF, "network"))
+    import params_help, filter_hub, data  # noqa
+    import models_att  # noqa
+    return params_help, filter_hub, data, models_att
+
+
+def ref_helpers():
+    params_help, filter_hub, data, models_att = _import_reference()
+    out = {}
+    for knn in range(1, 6):
+        out[f"neighbour_knn{knn}"] = params_help.get_neighbour_matrix_by_hand(
+            filter_hub.neighbour_dict_set[0], knn=knn)
+    import contextlib, io
+    with contextlib.redirect_stdout(io.StringIO()):
+        out["exp_matrix"] = models_att.get_exponential_matrix()
+    rng = np.random.default_rng(7)
+    x2 = rng.uniform(-1, 1, size=(5, 34))
+    x3 = rng.uniform(-1, 1, size=(5, 51))
+    out["flip_in2"], out["flip_out2"] = x2, data.flip_data(x2)
+    out["flip_in3"], out["flip_out3"] = x3, data.flip_data(x3)
+    out["rot_in2"], out["rot_out2"] = x2, data.rotate_data(x2, 180)
+    out["rot_in3"], out["rot_out3"] = x3, data.rotate_data(x3, 180)
+    out["rot_out3_90"] = data.rotate_data(x3, 90)
+    preds = rng.uniform(-1, 1, size=(4 * 5, 51))
+    out["undo_in"] = preds
+    out["undo_out_fr"] = data.undo(preds[:15], {"f": 1, "r": 2}, number_actions=2)
+    out["undo_out_frt"] = data.undo(preds, {"f": 1, "r": 2, "t": 3}, number_actions=3,
+                                    translation=0.05)
+    return out
+
+
+def notebook_masks():
+    res = {}
+    for fname, key in (("custom-dataset-h36m.ipynb", "nb_h36m_knn2"),
+                       ("custom-dataset-humansc3d.ipynb", "nb_humansc3d_knn1")):
+        nb = json.load(open(os.path.join(REF, "kaggle", fname)))
+        for cell in nb["cells"]:
+            txt = "".join("".join(o.get("text", [])) for o in cell.get("outputs", []))
+            k = txt.find("'neighbour_matrix': array(")
+            if k < 0:
+                continue
+            body = txt[k + len("'neighbour_matrix': array("):]
+            body = body[:body.index("dtype=float32)")]
+            nums = [float(v) for v in re.findall(r"[01]\.", body)]
+            res[key] = np.array(nums, np.float32).reshape(17, 17)
+            break
+    return res
+
+
+def notebook_facts():
+    facts = {}
+    nb = json.load(open(os.path.join(REF, "kaggle", "custom-dataset-h36m.ipynb")))
+    txt = "".join("".join(o.get("text", [])) for c in nb["cells"] for o in c.get("outputs", []))
+    m = re.search(r"Total steps to be done to complete all the epochs: (\d+)", txt)
+    facts["h36m_total_steps"] = int(m.group(1))
+    m = re.search(r"step (\d+) / \d+ \(epoch 1\.00 / 200\):\s+learning_rate = ([0-9.e+-]+)", txt)
+    facts["h36m_step1"], facts["h36m_lr1"] = int(m.group(1)), float(m.group(2))
+    facts["h36m_batch"], facts["h36m_epochs"] = 200, 200
+    nb = json.load(open(os.path.join(REF, "kaggle", "custom-dataset-humansc3d.ipynb")))
+    txt = "".join("".join(o.get("text", [])) for c in nb["cells"] for o in c.get("outputs", []))
+    m = re.search(r"Total steps to be done to complete all the epochs: (\d+)", txt)
+    facts["sc3d_total_steps"] = int(m.group(1))
+    m = re.search(r"step (\d+) / \d+ \(epoch 1\.00 / 100\):\s+learning_rate = ([0-9.e+-]+)", txt)
+    facts["sc3d_step1"], facts["sc3d_lr1"] = int(m.group(1)), float(m.group(2))
+    facts["sc3d_batch"], facts["sc3d_epochs"] = 512, 100
+    return facts
+
+
+def oracle_vectors():
+    """float64 oracle outputs for a few small configurations."""
+    cases = {
+        "lc_knn3_F8_L2_B24": dict(F=8, L=2, knn=3, B=24, mask="locally_connected", in_F=2),
+        "lc_knn1_F8_L1_B16_in3": dict(F=8, L=1, knn=1, B=16, mask="locally_connected", in_F=3),
+        "exp_F8_L1_B16": dict(F=8, L=1, knn=2, B=16, mask="exponential", in_F=2),
+        "lc_knn3_F64_L3_B32": dict(F=64, L=3, knn=3, B=32, mask="locally_connected", in_F=2),
+    }
+    res = {}
+    for name, c in cases.items():
+        cfg = O.Config(F=c["F"], in_F=c["in_F"], num_layers=c["L"], mask_type=c["mask"],
+                       neighbour=O.neighbour_matrix(c["knn"]))
+        params = O.init_params(cfg, seed=1)
+        rng = np.random.default_rng(2)
+        x = rng.uniform(-1, 1, size=(c["B"], 17 * c["in_F"])).astype(np.float32)
+        lab = rng.uniform(-1, 1, size=(c["B"], 51)).astype(np.float32)
+        out, cache = O.forward(cfg, params, x, np.float64)
+        grads = O.backward(cfg, params, cache, lab, np.float64)
+        d = {"x": x, "lab": lab, "out": out, "loss": np.float64(O.mse_loss(out, lab)),
+             "params_flat": O.flatten(cfg, params)}
+        d["grads_flat"] = np.concatenate([grads[n].ravel() for n, _ in O.param_specs(cfg)])
+        p2 = {k: v.copy() for k, v in params.items()}
+        st = O.adam_init(cfg, p2)
+        O.adam_step(cfg, p2, {k: v.astype(np.float32) for k, v in grads.items()}, st)
+        d["params_after_adam"] = O.flatten(cfg, p2)
+        if c["F"] > 16:
+            # full vectors would be tens of MB: keep per-tensor norms and a
+            # seeded sample of entries (params are re-created from seed=1)
+            sel = np.random.default_rng(3).choice(d["grads_flat"].size, 4096, replace=False)
+            d["sample_idx"] = sel
+            for k in ("grads_flat", "params_after_adam", "params_flat"):
+                d[k + "_sample"] = d.pop(k)[sel]
+            d["grad_norms"] = np.array([np.linalg.norm(grads[n]) for n, _ in O.param_specs(cfg)])
+        d["meta"] = np.array(json.dumps(c))
+        res[name] = d
+    return res
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    np.savez(os.path.join(OUT, "ref_helpers.npz"), **ref_helpers())
+    np.savez(os.path.join(OUT, "notebook_masks.npz"), **notebook_masks())
+    with open(os.path.join(OUT, "notebook_facts.json"), "w") as f:
+        json.dump(notebook_facts(), f, indent=1)
+    for name, d in oracle_vectors().items():
+        np.savez_compressed(os.path.join(OUT, f"oracle_{name}.npz"), **d)
+    print("wrote", sorted(os.listdir(OUT)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,515 @@
+"""CPU oracle for the LCN hot path -- TEST INFRASTRUCTURE ONLY.
+
+This module is the parity checker for the MI355X implementation in
+``lcn-pose_amd/``.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import it.  The product path never
+routes through it (``lcn_amd.native`` raises if the HIP library is missing).
+
+It is a plain-numpy restatement of the reference's locally-connected network
+(adgx/lcn-pose, ``network/models_att.py``).  Each function cites the reference
+lines it follows.  The reference executes its graph in TensorFlow 2.13.0, which
+is not vendored and not installed here, so the op semantics below restate TF's
+documented behaviour:
+
+* ``tf.clip_by_norm(t, 1)``       -> ``t * 1 / max(||t||_F, 1)``  (division, as TF)
+* ``tf.nn.softmax(V, axis=0)``    -> ``exp(V - max) / sum``
+* Keras ``BatchNormalization``    -> ``tf.nn.moments`` (two-pass, biased variance) and
+  ``tf.nn.batch_normalization``: ``inv = rsqrt(var + eps) * gamma``;
+  ``u = z * inv + (beta - mean * inv)``; eps = 1e-3; always batch statistics
+  (``training=self.is_training`` and ``is_training=True`` is hard-wired,
+  models_att.py:528, 667, 696, 737; train.py:107 -> params_help.py:170).
+* ``tf.nn.leaky_relu``            -> ``x > 0 ? x : 0.2 * x``
+* ``tf.nn.dropout(rate=0)``       -> identity
+* ``tf.compat.v1.train.AdamOptimizer`` (ApplyAdam kernel):
+  ``alpha = lr * sqrt(1 - b2^t) / (1 - b1^t)``; ``m += (g - m)(1 - b1)``;
+  ``v += (g^2 - v)(1 - b2)``; ``theta -= m * alpha / (sqrt(v) + eps)``
+* ``tf.compat.v1.train.exponential_decay(staircase=False)``:
+  ``lr * rate ** (global_step / decay_steps)`` in float32.
+
+Parity status: the arithmetic of the TF graph is **unpinned** (TF absent, no
+reference checkpoint or golden output exists).  The oracle is pinned on
+everything the reference itself can produce here: the knn neighbour matrices
+(reference helper + Kaggle notebook outputs), the exponential mask
+(reference helper), the flip/rotate/undo TTA helpers (reference helpers), the
+learning-rate schedule (values printed in the notebook logs); and it is
+cross-checked against float64 finite differences and torch autograd
+(``tests/test_oracle.py``).
+
+Layouts (joint-major, as the reference): activations ``a[b, j*F + f]``,
+input ``x[b, 2*j + c]``, output ``out[b, 3*j + c]``; weights ``W[i*Fin + p,
+j*Fout + q]`` with ``i`` the input joint and ``j`` the output joint
+(models_att.py:582).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+J = 17
+
+# tools/filter_hub.py:4-24 -- the H36M 17-joint skeleton adjacency.
+NEIGHBOUR_DICT = {
+    0: [1, 4, 7], 1: [0, 7, 2], 2: [1, 3], 3: [2], 4: [0, 7, 5], 5: [4, 6],
+    6: [5], 7: [1, 0, 4, 14, 8, 11], 8: [7, 9, 11, 14], 9: [8, 10], 10: [9],
+    11: [8, 7, 12], 12: [11, 13], 13: [12], 14: [8, 7, 15], 15: [14, 16],
+    16: [15],
+}
+
+# models_att.py:19-36 -- the edge list of get_exponential_matrix (18 edges; it
+# lacks 8-11 and 8-14 compared with filter_hub, which is reproduced as is).
+EXP_EDGES = [(0, 1), (0, 7), (0, 4), (4, 5), (4, 7), (5, 6), (1, 7), (1, 2),
+             (2, 3), (7, 11), (7, 8), (7, 14), (11, 12), (12, 13), (14, 15),
+             (15, 16), (8, 9), (9, 10)]
+
+
+def neighbour_matrix(knn: int = 1) -> np.ndarray:
+    """tools/params_help.py:8-20 (get_neighbour_matrix_by_hand)."""
+    n = np.zeros((J, J), dtype=np.float32)
+    for idx in range(J):
+        n[idx, [idx] + NEIGHBOUR_DICT[idx]] = 1
+    if knn >= 2:
+        n = np.linalg.matrix_power(n, knn)
+        n = np.array(n != 0, dtype=np.float32)
+    return n
+
+
+def exponential_matrix() -> np.ndarray:
+    """models_att.py:14-69 (get_exponential_matrix), without its prints."""
+    dist = np.full((J, J), np.inf)
+    np.fill_diagonal(dist, 0)
+    for u, v in EXP_EDGES:
+        dist[u][v] = 1
+        dist[v][u] = 1
+    for k in range(J):
+        for i in range(J):
+            for j in range(J):
+                if dist[i, j] > dist[i, k] + dist[k, j]:
+                    dist[i, j] = dist[i, k] + dist[k, j]
+    return (1 / (2 ** dist)).astype(np.float32)
+
+
+@dataclasses.dataclass
+class Config:
+    """Subset of cgcnn(**params) (models_att.py:478-532) that shapes the math."""
+    F: int = 64
+    in_F: int = 2
+    num_layers: int = 3
+    mask_type: str = "locally_connected"
+    neighbour: Optional[np.ndarray] = None      # [17,17]; LC structure N
+    residual: bool = True
+    batch_norm: bool = True
+    max_norm: bool = True
+    regularization: Optional[float] = 0.0
+    learning_rate: float = 1e-3
+    decay_steps: int = 32000
+    decay_rate: float = 0.96
+    bn_eps: float = 1e-3
+    leaky_alpha: float = 0.2
+    beta1: float = 0.9
+    beta2: float = 0.999
+    adam_eps: float = 1e-8
+
+    @property
+    def learnable_mask(self) -> bool:
+        return "locally_connected" in self.mask_type
+
+    @property
+    def H(self) -> int:
+        return J * self.F
+
+
+def param_specs(cfg: Config) -> List[Tuple[str, Tuple[int, ...]]]:
+    """Canonical parameter order = TF variable creation order.
+
+    mask (models_att.py:557) -> w1, b1 (:714, :721) -> BN0 gamma/beta (:736) ->
+    per block l: w2_l, b2_l, BN1l, w3_l, b3_l, BN2l (:647-698) -> w4, b4 (:750-761).
+    Only trainable variables are listed (BN moving statistics are never used,
+    because BN always runs in training mode).
+    """
+    H, F, in_F = cfg.H, cfg.F, cfg.in_F
+    specs: List[Tuple[str, Tuple[int, ...]]] = []
+    if cfg.learnable_mask:
+        specs.append(("mask", (J, J)))
+    specs += [("w1", (J * in_F, H)), ("b1", (H,))]
+    if cfg.batch_norm:
+        specs += [("bn0_gamma", (F,)), ("bn0_beta", (F,))]
+    for l in range(cfg.num_layers):
+        specs += [(f"w2_{l}", (H, H)), (f"b2_{l}", (H,))]
+        if cfg.batch_norm:
+            specs += [(f"bn1{l}_gamma", (F,)), (f"bn1{l}_beta", (F,))]
+        specs += [(f"w3_{l}", (H, H)), (f"b3_{l}", (H,))]
+        if cfg.batch_norm:
+            specs += [(f"bn2{l}_gamma", (F,)), (f"bn2{l}_beta", (F,))]
+    specs += [("w4", (H, J * 3)), ("b4", (J * 3,))]
+    return specs
+
+
+def layer_names(cfg: Config) -> List[Tuple[str, str, Optional[str], int, int]]:
+    """(weight, bias, bn-prefix, Fin, Fout) per linear layer, in forward order."""
+    out = [("w1", "b1", "bn0" if cfg.batch_norm else None, cfg.in_F, cfg.F)]
+    for l in range(cfg.num_layers):
+        out.append((f"w2_{l}", f"b2_{l}", f"bn1{l}" if cfg.batch_norm else None, cfg.F, cfg.F))
+        out.append((f"w3_{l}", f"b3_{l}", f"bn2{l}" if cfg.batch_norm else None, cfg.F, cfg.F))
+    out.append(("w4", "b4", None, cfg.F, 3))
+    return out
+
+
+def truncated_normal(rng: np.random.Generator, shape) -> np.ndarray:
+    """tf.random.truncated_normal(mean 0, stddev 1): redraw outside 2 sigma."""
+    out = rng.standard_normal(size=shape)
+    bad = np.abs(out) > 2.0
+    while bad.any():
+        out[bad] = rng.standard_normal(size=int(bad.sum()))
+        bad = np.abs(out) > 2.0
+    return out
+
+
+def init_params(cfg: Config, seed: int = 0) -> Dict[str, np.ndarray]:
+    """cgcnn.kaiming (models_att.py:614-628): trunc_normal * sqrt(2/shape[0]).
+
+    Biases use shape[0] = len(b).  The mask starts at N^T (init_type 'same',
+    :549-566); BN gamma = 1, beta = 0 (Keras defaults).
+    """
+    rng = np.random.default_rng(seed)
+    p: Dict[str, np.ndarray] = {}
+    for name, shape in param_specs(cfg):
+        if name == "mask":
+            p[name] = np.array(cfg.neighbour, dtype=np.float32).T.copy()
+        elif name.endswith("_gamma"):
+            p[name] = np.ones(shape, np.float32)
+        elif name.endswith("_beta"):
+            p[name] = np.zeros(shape, np.float32)
+        else:
+            p[name] = (truncated_normal(rng, shape) * math.sqrt(2.0 / shape[0])).astype(np.float32)
+    return p
+
+
+def flatten(cfg: Config, params: Dict[str, np.ndarray]) -> np.ndarray:
+    return np.concatenate([np.asarray(params[n], np.float32).ravel() for n, _ in param_specs(cfg)])
+
+
+def unflatten(cfg: Config, flat: np.ndarray) -> Dict[str, np.ndarray]:
+    out, off = {}, 0
+    for n, shape in param_specs(cfg):
+        size = int(np.prod(shape))
+        out[n] = flat[off:off + size].reshape(shape)
+        off += size
+    assert off == flat.size
+    return out
+
+
+# ----------------------------------------------------------------------------
+# Mask and weight preparation
+# ----------------------------------------------------------------------------
+
+def structure(cfg: Config) -> np.ndarray:
+    """C = 1[L != 0] with L = N^T (models_att.py:549, 571); row i = input joint."""
+    if cfg.learnable_mask:
+        return (np.asarray(cfg.neighbour).T != 0).astype(np.float32)
+    return np.ones((J, J), np.float32)
+
+
+def mask_value(cfg: Config, params, dtype=np.float32) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+    """models_att.py:547-574.  Returns (M, S) with S = softmax(V, 0) (LC only)."""
+    if cfg.learnable_mask:
+        V = params["mask"].astype(dtype)
+        e = np.exp(V - V.max(axis=0, keepdims=True))
+        S = e / e.sum(axis=0, keepdims=True)
+        return S * structure(cfg).astype(dtype), S
+    return exponential_matrix().astype(dtype), None
+
+
+def effective_weight(cfg: Config, W: np.ndarray, M: np.ndarray, Fin: int, Fout: int):
+    """clip_by_norm (models_att.py:659/690/726/762) then mask_weights (:576-586).
+
+    Returns (W_e, W_c, norm)."""
+    n = np.sqrt(np.sum(W * W, dtype=W.dtype))
+    if cfg.max_norm:
+        Wc = (W * W.dtype.type(1)) / max(n, W.dtype.type(1))
+    else:
+        Wc = W
+    We = (Wc.reshape(J, Fin, J, Fout) * M.reshape(J, 1, J, 1)).reshape(W.shape)
+    return We, Wc, n
+
+
+# ----------------------------------------------------------------------------
+# Forward
+# ----------------------------------------------------------------------------
+
+def _bn_forward(cfg: Config, z, gamma, beta, F):
+    """batch_normalization_warp (models_att.py:588-612) in training mode."""
+    B = z.shape[0]
+    z3 = z.reshape(B, J, F)
+    mean = z3.mean(axis=(0, 1))
+    var = ((z3 - mean) ** 2).mean(axis=(0, 1))
+    rstd = 1.0 / np.sqrt(var + z.dtype.type(cfg.bn_eps))
+    inv = rstd * gamma
+    u = z3 * inv + (beta - mean * inv)
+    return u.reshape(B, -1), dict(mean=mean, var=var, rstd=rstd, inv=inv)
+
+
+def _act(cfg, u):
+    return np.where(u > 0, u, u * u.dtype.type(cfg.leaky_alpha))
+
+
+def forward(cfg: Config, params, x: np.ndarray, dtype=np.float32, keep: bool = True):
+    """_inference_lcn (models_att.py:707-775).  Returns (out, cache)."""
+    P = {k: np.asarray(v, dtype) for k, v in params.items()}
+    x = np.asarray(x, dtype)
+    B = x.shape[0]
+    M, S = mask_value(cfg, P, dtype)
+    layers = layer_names(cfg)
+    eff = {}
+    for (wn, bn, bnp, fin, fout) in layers:
+        eff[wn] = effective_weight(cfg, P[wn], M, fin, fout)
+    cache = dict(M=M, S=S, eff=eff, x=x, layers=[])
+
+    def linear_bn_act(a, li):
+        wn, bname, bnp, fin, fout = layers[li]
+        z = a @ eff[wn][0] + P[bname]
+        if bnp is not None:
+            u, st = _bn_forward(cfg, z, P[bnp + "_gamma"], P[bnp + "_beta"], fout)
+        else:
+            u, st = z, None
+        h = _act(cfg, u)
+        if keep:
+            cache["layers"].append(dict(a=a, z=z, u=u, st=st))
+        return h, z, st
+
+    h, _, _ = linear_bn_act(x, 0)                          # :729-742
+    li = 1
+    block_in = []
+    for l in range(cfg.num_layers):                        # :745-746
+        hin = h
+        g, _, _ = linear_bn_act(hin, li)                   # :662-673
+        t, _, _ = linear_bn_act(g, li + 1)                 # :692-700
+        h = hin + t if cfg.residual else t                 # :704
+        block_in.append(hin)
+        li += 2
+    wn, bname, _, _, _ = layers[-1]
+    y = h @ eff[wn][0] + P[bname]                          # :765
+    if keep:
+        cache["hL"] = h
+        cache["block_in"] = block_in
+    x3 = x.reshape(B, J, cfg.in_F)
+    y3 = y.reshape(B, J, 3)
+    out = np.concatenate([x3[:, :, :2] + y3[:, :, :2], y3[:, :, 2:3]], axis=2)  # :768-773
+    return out.reshape(B, J * 3), cache
+
+
+def mse_loss(out: np.ndarray, lab: np.ndarray) -> float:
+    """base_model.loss (models_att.py:356)."""
+    d = out - np.asarray(lab, out.dtype)
+    return float(np.mean(d * d))
+
+
+def reg_loss(cfg: Config, params, dtype=np.float64) -> float:
+    """models_att.py:362-365 + _variable (:465-472): reg * sum(l2_loss(W, b))."""
+    if cfg.regularization in (0, None):
+        return 0.0
+    tot = 0.0
+    for (wn, bn, _, _, _) in layer_names(cfg):
+        tot += float(np.sum(np.asarray(params[wn], dtype) ** 2) / 2)
+        tot += float(np.sum(np.asarray(params[bn], dtype) ** 2) / 2)
+    return cfg.regularization * tot
+
+
+# ----------------------------------------------------------------------------
+# Backward (analytic)
+# ----------------------------------------------------------------------------
+
+def _bn_act_backward(cfg, dh, rec, F, gamma):
+    B = dh.shape[0]
+    u = rec["u"]
+    du = dh * np.where(u > 0, dh.dtype.type(1), dh.dtype.type(cfg.leaky_alpha))
+    st = rec["st"]
+    if st is None:
+        return du, None, None
+    N = B * J
+    z3 = rec["z"].reshape(B, J, F)
+    zhat = (z3 - st["mean"]) * st["rstd"]
+    du3 = du.reshape(B, J, F)
+    S1 = du3.sum(axis=(0, 1))
+    S2 = (du3 * zhat).sum(axis=(0, 1))
+    dz = (gamma * st["rstd"] / N) * (N * du3 - S1 - zhat * S2)
+    return dz.reshape(B, -1), S2, S1
+
+
+def backward(cfg: Config, params, cache, lab: np.ndarray, dtype=np.float32,
+             global_batch: Optional[int] = None) -> Dict[str, np.ndarray]:
+    """Gradients of the MSE loss (+ regularisation) w.r.t. every trainable.
+
+    ``global_batch`` lets a shard scale its loss gradient by the global batch
+    (data-parallel decomposition tests)."""
+    P = {k: np.asarray(v, dtype) for k, v in params.items()}
+    layers = layer_names(cfg)
+    eff = cache["eff"]
+    B = cache["x"].shape[0]
+    Bg = B if global_batch is None else global_batch
+    out, _ = None, None
+    hL = cache["hL"]
+    wn4, bn4, _, _, _ = layers[-1]
+    y = hL @ eff[wn4][0] + P[bn4]
+    x3 = cache["x"].reshape(B, J, cfg.in_F)
+    y3 = y.reshape(B, J, 3)
+    out = np.concatenate([x3[:, :, :2] + y3[:, :, :2], y3[:, :, 2:3]], axis=2).reshape(B, -1)
+    dy = (dtype(2.0) / dtype(Bg * J * 3)) * (out - np.asarray(lab, dtype))
+    g: Dict[str, np.ndarray] = {}
+    dWe = {}
+    dWe[wn4] = hL.T @ dy
+    g[bn4] = dy.sum(axis=0)
+    dh = dy @ eff[wn4][0].T
+
+    recs = cache["layers"]
+    li = len(layers) - 2
+    for l in reversed(range(cfg.num_layers)):
+        dres = dh
+        # second linear of block l (layer li)
+        for k in (li, li - 1):
+            wn, bname, bnp, fin, fout = layers[k]
+            rec = recs[k]
+            gamma = P[bnp + "_gamma"] if bnp else None
+            dz, dgam, dbet = _bn_act_backward(cfg, dh, rec, fout, gamma)
+            if bnp:
+                g[bnp + "_gamma"], g[bnp + "_beta"] = dgam, dbet
+            dWe[wn] = rec["a"].T @ dz
+            g[bname] = dz.sum(axis=0)
+            dh = dz @ eff[wn][0].T
+        if cfg.residual:
+            dh = dh + dres
+        li -= 2
+    wn, bname, bnp, fin, fout = layers[0]
+    rec = recs[0]
+    gamma = P[bnp + "_gamma"] if bnp else None
+    dz, dgam, dbet = _bn_act_backward(cfg, dh, rec, fout, gamma)
+    if bnp:
+        g[bnp + "_gamma"], g[bnp + "_beta"] = dgam, dbet
+    dWe[wn] = rec["a"].T @ dz
+    g[bname] = dz.sum(axis=0)
+
+    # mask / clip backward
+    M, S = cache["M"], cache["S"]
+    dM = np.zeros((J, J), dtype)
+    for (wn, bname, _, fin, fout) in layers:
+        We, Wc, n = eff[wn]
+        d4 = dWe[wn].reshape(J, fin, J, fout)
+        dWc = (d4 * M.reshape(J, 1, J, 1)).reshape(We.shape)
+        dM += (d4 * Wc.reshape(J, fin, J, fout)).sum(axis=(1, 3))
+        W = P[wn]
+        if cfg.max_norm and n > 1:
+            dW = dWc / n - (np.sum(dWc * W) / (n ** 3)) * W
+        else:
+            dW = dWc
+        g[wn] = dW
+    if cfg.regularization not in (0, None):
+        for (wn, bname, _, _, _) in layers:
+            g[wn] = g[wn] + dtype(cfg.regularization) * P[wn]
+            g[bname] = g[bname] + dtype(cfg.regularization) * P[bname]
+    if cfg.learnable_mask:
+        C = structure(cfg).astype(dtype)
+        dS = dM * C
+        g["mask"] = S * (dS - (S * dS).sum(axis=0, keepdims=True))
+    return {k: np.asarray(v, dtype) for k, v in g.items()}
+
+
+# ----------------------------------------------------------------------------
+# Optimiser
+# ----------------------------------------------------------------------------
+
+def learning_rate(cfg: Config, global_step: int) -> np.float32:
+    """exponential_decay(lr, global_step, 32000, 0.96, staircase=False)
+    (models_att.py:392-399, params_help.py:129-130), float32 arithmetic."""
+    p = np.float32(global_step) / np.float32(cfg.decay_steps)
+    return np.float32(np.float32(cfg.learning_rate) * np.power(np.float32(cfg.decay_rate), p))
+
+
+@dataclasses.dataclass
+class AdamState:
+    m: Dict[str, np.ndarray]
+    v: Dict[str, np.ndarray]
+    global_step: int = 0
+    beta1_power: np.float32 = np.float32(0.9)
+    beta2_power: np.float32 = np.float32(0.999)
+
+
+def adam_init(cfg: Config, params) -> AdamState:
+    return AdamState({k: np.zeros_like(v, np.float32) for k, v in params.items()},
+                     {k: np.zeros_like(v, np.float32) for k, v in params.items()},
+                     0, np.float32(cfg.beta1), np.float32(cfg.beta2))
+
+
+def adam_step(cfg: Config, params, grads, st: AdamState):
+    """AdamOptimizer.apply_gradients (models_att.py:404-409), in place.
+
+    Returns the learning rate used (what op_train returns, :419-420)."""
+    lr = learning_rate(cfg, st.global_step)
+    b1, b2, eps = np.float32(cfg.beta1), np.float32(cfg.beta2), np.float32(cfg.adam_eps)
+    alpha = np.float32(lr * np.sqrt(np.float32(1) - st.beta2_power) / (np.float32(1) - st.beta1_power))
+    for k in params:
+        gk = np.asarray(grads[k], np.float32)
+        m, v = st.m[k], st.v[k]
+        m += (gk - m) * (np.float32(1) - b1)
+        v += (gk * gk - v) * (np.float32(1) - b2)
+        params[k] = (params[k] - (m * alpha) / (np.sqrt(v) + eps)).astype(np.float32)
+    st.beta1_power = np.float32(st.beta1_power * b1)
+    st.beta2_power = np.float32(st.beta2_power * b2)
+    st.global_step += 1
+    return lr
+
+
+def train_step(cfg: Config, params, st: AdamState, x, lab, dtype=np.float32):
+    """One op_train (models_att.py:382-421): forward, loss, grads, Adam."""
+    out, cache = forward(cfg, params, x, dtype)
+    loss = mse_loss(out, lab) + reg_loss(cfg, params)
+    grads = backward(cfg, params, cache, lab, dtype)
+    lr = adam_step(cfg, params, grads, st)
+    return loss, lr, grads
+
+
+# ----------------------------------------------------------------------------
+# Test-time augmentation helpers (tools/data.py)
+# ----------------------------------------------------------------------------
+
+LEFT = [4, 5, 6, 11, 12, 13]
+RIGHT = [1, 2, 3, 14, 15, 16]
+
+
+def flip_data(data: np.ndarray) -> np.ndarray:
+    """tools/data.py:10-25."""
+    f = data.copy().reshape((len(data), J, -1))
+    f[:, :, 0] *= -1
+    f[:, LEFT + RIGHT] = f[:, RIGHT + LEFT]
+    return f.reshape(data.shape)
+
+
+def rotate_data(data: np.ndarray, angle: float = 180) -> np.ndarray:
+    """tools/data.py:289-322 (2-D uses Rz.T[:2,:2]; 3-D rotates about joint 0)."""
+    th = np.radians(angle)
+    Rz = np.array([[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1]])
+    r = data.copy().reshape((len(data), J, -1)).astype(np.float64)
+    k = r.shape[2]
+    piv = r[:, 0:1, :min(k, 3)].copy()
+    if k == 2:
+        r = (r - piv) @ Rz.T[:2, :2] + piv
+    else:
+        r[:, :, :3] = (r[:, :, :3] - piv) @ Rz.T + piv
+    return r.reshape(data.shape).astype(data.dtype)
+
+
+def undo(preds: np.ndarray, op_ord: dict, number_actions: int, angle: float = 180,
+         translation: float = 0.5) -> np.ndarray:
+    """tools/data.py:269-287 (unflip :236-249, rotate, untranslate :205-218)."""
+    d = preds.copy().reshape(number_actions + 1, -1, J, 3)
+    if "f" in op_ord:
+        u = d[op_ord["f"]].copy()
+        u[:, :, 0] *= -1
+        u[:, LEFT + RIGHT] = u[:, RIGHT + LEFT]
+        d[op_ord["f"]] = u
+    if "r" in op_ord:
+        d[op_ord["r"]] = rotate_data(d[op_ord["r"]], angle)
+    if "t" in op_ord:
+        d[op_ord["t"]] = d[op_ord["t"]] - translation
+    return d.mean(axis=0).reshape(-1, J * 3)
