@@ -1,0 +1,136 @@
+/*
+ * lcn.h -- C ABI of liblcn.so, the MI355X-native locally-connected network
+ * (LCN) hot path of adgx/lcn-pose.
+ *
+ * The reference's hot path is the TensorFlow graph built by
+ * network/models_att.py (cgcnn._inference_lcn :707-775, base_model.loss
+ * :352-380, base_model.training :382-421) and driven by one
+ * tf.compat.v1.Session.run per step (fit :210-212, predict :112-121).  This
+ * library replaces that graph + Session: every op of the forward, backward
+ * and Adam update runs in hand-written HIP kernels for gfx950.  The Python
+ * class network.models_att.cgcnn (lcn-pose_amd/network/models_att.py) keeps
+ * the reference's API and calls these entry points through ctypes.
+ *
+ * Conventions
+ *   - every function returns 0 on success, a negative LCN_E* code on error;
+ *     lcn_last_error(h) (or lcn_last_error(NULL) for lcn_create failures)
+ *     returns a message;
+ *   - host buffers are C-contiguous float32 owned by the caller; device
+ *     buffers are owned by the handle; one HIP stream per handle; a handle
+ *     is not thread-safe (one handle per GPU, one process per GPU);
+ *   - layouts are the reference's: input x[b, in_F*j + c], labels and
+ *     output [b, 3*j + c]; flat parameters in TF variable-creation order
+ *     (mask, w1, b1, bn gamma/beta, per block w2,b2,bn1,w3,b3,bn2, w4, b4),
+ *     each tensor row-major as in the reference (W[i*Fin+p, j*Fout+q]).
+ */
+#ifndef LCN_H
+#define LCN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LCN_ABI_VERSION 1
+
+enum {
+  LCN_OK = 0,
+  LCN_E_ARG = -1,      /* bad argument / shape                       */
+  LCN_E_HIP = -2,      /* HIP runtime error                          */
+  LCN_E_NOMEM = -3,    /* device allocation failed                   */
+  LCN_E_COMM = -4,     /* RCCL error                                 */
+  LCN_E_STATE = -5     /* call not valid in the current state        */
+};
+
+/* mask kinds: cgcnn._initialize_mask (models_att.py:547-574) */
+enum { LCN_MASK_LOCALLY_CONNECTED = 0, LCN_MASK_EXPONENTIAL = 1 };
+
+/* flags for lcn_forward / lcn_train_step */
+enum {
+  LCN_IN_DEVICE = 1,      /* x / labels are device pointers (e.g. lcn_device_buffer) */
+  LCN_OUT_DEVICE = 2,     /* out is a device pointer                                  */
+  LCN_NO_UPDATE = 4,      /* train_step: compute gradients, skip the Adam update      */
+  LCN_KEEP_GRADS = 8,     /* train_step: keep final dense gradients (lcn_get_grads)   */
+  LCN_ASYNC = 16          /* do not synchronise the stream before returning           */
+};
+
+typedef struct lcn_config {
+  int32_t abi_version;     /* = LCN_ABI_VERSION                                  */
+  int32_t joints;          /* in_joints == out_joints == 17 (models_att.py:512-513) */
+  int32_t in_f;            /* in_F, 2 or 3                                       */
+  int32_t f;               /* F channels per joint, multiple of 64               */
+  int32_t num_layers;      /* two_linear blocks                                  */
+  int32_t mask_type;       /* LCN_MASK_*                                         */
+  int32_t residual;        /* models_att.py:704                                  */
+  int32_t batch_norm;      /* models_att.py:664, 693, 732                        */
+  int32_t max_norm;        /* clip_by_norm(w, 1), models_att.py:659, 690, 726, 762 */
+  int32_t reserved0;
+  float bn_eps;            /* Keras BN epsilon, 1e-3                             */
+  float leaky_alpha;       /* tf.nn.leaky_relu alpha, 0.2                        */
+  float regularization;    /* 0 = off (models_att.py:362)                        */
+  float learning_rate;     /* exponential_decay (models_att.py:392-399)          */
+  float decay_rate;
+  float beta1, beta2, adam_eps;
+  int64_t decay_steps;
+  int64_t max_batch;       /* largest per-call batch on this GPU                 */
+  /* joints x joints, row = input joint i, column = output joint j:
+   *   LC:  structure C[i][j] = (N^T)[i][j] != 0 (models_att.py:549, 571)
+   *   EXP: the constant mask 2^-d (models_att.py:61, 574)                      */
+  const float* mask_matrix;
+} lcn_config;
+
+/* --- lifetime --------------------------------------------------------- */
+int lcn_create(const lcn_config* cfg, int device, void** handle);
+int lcn_destroy(void* handle);
+const char* lcn_last_error(void* handle);
+int lcn_abi_version(void);
+
+/* --- parameters / optimiser state (checkpoint I/O) ------------------- */
+int64_t lcn_num_params(void* handle);
+int lcn_param_layout(void* handle, int32_t index, char* name, int32_t name_cap,
+                     int64_t* offset, int64_t* rows, int64_t* cols);
+int lcn_set_params(void* handle, const float* flat, int64_t n);
+int lcn_get_params(void* handle, float* flat, int64_t n);
+int lcn_set_optimizer_state(void* handle, const float* m, const float* v, int64_t n,
+                            int64_t global_step, float beta1_power, float beta2_power);
+int lcn_get_optimizer_state(void* handle, float* m, float* v, int64_t n,
+                            int64_t* global_step, float* beta1_power, float* beta2_power);
+int lcn_get_grads(void* handle, float* flat, int64_t n);
+
+/* --- compute ----------------------------------------------------------- */
+/* predict one batch (models_att.py:79-132 inner body): out[B, 3*joints] */
+int lcn_forward(void* handle, const float* x, float* out, int64_t batch, int32_t flags);
+/* forward + mean-squared loss (predict with labels, models_att.py:108-115) */
+int lcn_forward_loss(void* handle, const float* x, const float* labels, float* out,
+                     int64_t batch, int32_t flags, float* loss);
+/* one op_train (models_att.py:382-421): forward, loss, backward, Adam.
+ * loss_out / lr_out may be NULL (then nothing is copied back). */
+int lcn_train_step(void* handle, const float* x, const float* labels, int64_t batch,
+                   int32_t flags, float* loss_out, float* lr_out);
+int lcn_synchronize(void* handle);
+
+/* --- device-resident data (on-device datasets; no host copies per step) */
+int lcn_device_buffer(void* handle, int32_t slot, int64_t bytes, void** dptr);
+int lcn_memcpy_h2d(void* handle, void* dst, const void* src, int64_t bytes);
+int lcn_memcpy_d2h(void* handle, void* dst, const void* src, int64_t bytes);
+
+/* --- data parallel (RCCL over xGMI) ------------------------------------ */
+int lcn_comm_unique_id(void* id_out /* 128 bytes */);
+int lcn_comm_init(void* handle, const void* id /* 128 bytes */, int32_t rank, int32_t world);
+int lcn_comm_allreduce_host(void* handle, double* values, int32_t count, int32_t op /* 0 sum, 1 max */);
+
+/* --- instrumentation --------------------------------------------------- */
+/* kernel ids for lcn_kernel_timing */
+enum { LCN_K_GEMM_FWD = 0, LCN_K_GEMM_DX = 1, LCN_K_GEMM_DW = 2, LCN_K_NUM = 3 };
+int lcn_set_timing(void* handle, int32_t enable);
+int lcn_kernel_timing(void* handle, int32_t kernel, int64_t* launches, double* total_ms,
+                      double* flops);
+/* debug: copy an internal activation to host.  kind 0 = z (pre-BN) of linear
+ * layer idx, 1 = block output h_idx, 2 = BN (mean, rstd) of BN layer idx */
+int lcn_debug_tensor(void* handle, int32_t kind, int32_t idx, float* host, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LCN_H */

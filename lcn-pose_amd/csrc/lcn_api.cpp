@@ -1,0 +1,1035 @@
+// liblcn.so host side: the C ABI of include/lcn.h, device memory plan and the
+// per-step kernel schedule that replaces the reference's TF graph + Session.
+//
+//   forward  (cgcnn._inference_lcn, models_att.py:707-775)
+//   loss     (base_model.loss, :352-380)
+//   backward (optimizer.compute_gradients, :408) + Adam (:404-409)
+//
+// One HIP stream per handle; every launch is stream-ordered, the host only
+// synchronises when a result is copied back.  With world > 1 (one process per
+// GPU) the data-parallel exchanges are RCCL all-reduces on the same stream:
+// SyncBN statistics (the reference BN always uses whole-batch statistics) and
+// one all-reduce of the raw gradient vector per step.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/lcn.h"
+#include "lcn_internal.h"
+
+using namespace lcn;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct ParamSpec {
+  std::string name;
+  int64_t off, rows, cols;
+};
+
+struct Timer {
+  std::vector<hipEvent_t> ev;  // start/stop pairs
+  int64_t launches = 0;
+  double flops = 0, ms = 0;
+};
+
+struct Handle {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  // configuration
+  int inF = 2, F = 64, L = 3, H = 0, spj = 1, nslab = 0, nl = 0, nbn = 0;
+  int learnable = 1, residual = 1, batch_norm = 1, max_norm = 1;
+  float eps = 1e-3f, alpha = 0.2f, reg = 0.f, lr0 = 1e-3f, decay_rate = 0.96f;
+  float b1 = 0.9f, b2 = 0.999f, adam_eps = 1e-8f;
+  int64_t decay_steps = 32000, Bmax = 0;
+  std::vector<float> Cmat;  // host copy [17*17]
+
+  // parameters / optimiser
+  int64_t P = 0;
+  std::vector<ParamSpec> specs;
+  float *theta = nullptr, *m = nullptr, *v = nullptr, *rg = nullptr, *gout = nullptr;
+  int64_t global_step = 0;
+  float b1p = 0.9f, b2p = 0.999f;
+  int grads_valid = 0;
+
+  // layers
+  std::vector<WLayer> wl;
+  std::vector<int64_t> b_off, gamma_off, beta_off;  // per linear layer (-1 if none)
+  int64_t mask_off = -1;
+
+  // block structure of the hidden layers (64-granular slabs)
+  int nblk = 0;
+  int *fwd_ptr = nullptr, *bwd_ptr = nullptr;
+  int2 *fwd_idx = nullptr, *bwd_idx = nullptr, *blk = nullptr;
+  unsigned *umask_lift = nullptr, *umask_out = nullptr;
+
+  // mask / norms
+  float *Md = nullptr, *Sd = nullptr, *Cd = nullptr, *denom = nullptr, *lcoef = nullptr;
+  double *norm_part = nullptr, *norm2 = nullptr, *blocksum = nullptr;
+  int64_t *w_offs = nullptr, *w_sizes = nullptr;
+  int *w_kin = nullptr, *w_nout = nullptr;
+  int norm_ppl = 64;
+
+  // activations
+  float *x = nullptr, *lab = nullptr, *out = nullptr, *dy = nullptr;
+  std::vector<float*> Z, Hb;
+  float *DH = nullptr, *DZ = nullptr, *DG = nullptr;
+  std::vector<BnStats> bn;
+  float *ident_scale = nullptr, *ident_shift = nullptr, *ident_c123 = nullptr;
+  float* c123 = nullptr;
+  float2* stat_part = nullptr;
+  float *bpart = nullptr, *dw_part = nullptr, *outer_part = nullptr, *col_part = nullptr;
+  double *loss_part = nullptr, *loss_sum = nullptr, *acc1 = nullptr, *acc2 = nullptr;
+  int dw_nch_max = 1, outer_nch_max = 1;
+
+  // Adam segments
+  AdamSeg* segs = nullptr;
+  int64_t* seg_start = nullptr;
+  int nseg = 0;
+  int64_t adam_blocks = 0;
+
+  // last batch
+  int64_t lastB = 0;
+
+  // user device buffers
+  std::vector<void*> user_bufs;
+  std::vector<int64_t> user_bytes;
+
+  // communication
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1;
+
+  // instrumentation
+  int timing = 0;
+  Timer timers[LCN_K_NUM];
+
+  std::vector<void*> allocs;
+};
+
+#define HIPC(expr)                                                                   \
+  do {                                                                               \
+    hipError_t e_ = (expr);                                                          \
+    if (e_ != hipSuccess) {                                                          \
+      h->err = std::string(#expr) + ": " + hipGetErrorString(e_);                    \
+      return LCN_E_HIP;                                                              \
+    }                                                                                \
+  } while (0)
+
+#define NCCLC(expr)                                                                  \
+  do {                                                                               \
+    ncclResult_t r_ = (expr);                                                        \
+    if (r_ != ncclSuccess) {                                                         \
+      h->err = std::string(#expr) + ": " + ncclGetErrorString(r_);                   \
+      return LCN_E_COMM;                                                             \
+    }                                                                                \
+  } while (0)
+
+#define CHECK(expr)                                                                  \
+  do {                                                                               \
+    int rc_ = (expr);                                                                \
+    if (rc_ != LCN_OK) return rc_;                                                   \
+  } while (0)
+
+template <typename T>
+int dalloc(Handle* h, T** p, size_t count) {
+  void* q = nullptr;
+  hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T));
+  if (e != hipSuccess) {
+    h->err = "hipMalloc(" + std::to_string(count * sizeof(T)) + " bytes): " + hipGetErrorString(e);
+    return LCN_E_NOMEM;
+  }
+  hipMemset(q, 0, std::max<size_t>(count, 1) * sizeof(T));
+  h->allocs.push_back(q);
+  *p = (T*)q;
+  return LCN_OK;
+}
+
+template <typename T>
+int upload(Handle* h, T** p, const std::vector<T>& src) {
+  CHECK(dalloc(h, p, src.size()));
+  HIPC(hipMemcpy(*p, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+  return LCN_OK;
+}
+
+int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------------------
+// construction
+// ---------------------------------------------------------------------------
+int build(Handle* h, const lcn_config* c) {
+  h->inF = c->in_f;
+  h->F = c->f;
+  h->L = c->num_layers;
+  h->H = kJ * h->F;
+  h->spj = h->F / kSlab;
+  h->nslab = kJ * h->spj;
+  h->nl = 2 * h->L + 2;
+  h->learnable = c->mask_type == LCN_MASK_LOCALLY_CONNECTED;
+  h->residual = c->residual;
+  h->batch_norm = c->batch_norm;
+  h->max_norm = c->max_norm;
+  h->eps = c->bn_eps;
+  h->alpha = c->leaky_alpha;
+  h->reg = c->regularization;
+  h->lr0 = c->learning_rate;
+  h->decay_rate = c->decay_rate;
+  h->decay_steps = c->decay_steps;
+  h->b1 = c->beta1;
+  h->b2 = c->beta2;
+  h->adam_eps = c->adam_eps;
+  h->b1p = h->b1;
+  h->b2p = h->b2;
+  h->Bmax = c->max_batch;
+  h->Cmat.assign(c->mask_matrix, c->mask_matrix + kJ * kJ);
+  const int H = h->H, F = h->F, inF = h->inF, nl = h->nl;
+
+  // ---- parameter layout (TF variable creation order) ----
+  int64_t off = 0;
+  auto add = [&](const std::string& n, int64_t r, int64_t cc) {
+    h->specs.push_back({n, off, r, cc});
+    off += r * cc;
+    return off - r * cc;
+  };
+  if (h->learnable) h->mask_off = add("mask", kJ, kJ);
+  h->b_off.assign(nl, -1);
+  h->gamma_off.assign(nl, -1);
+  h->beta_off.assign(nl, -1);
+  h->wl.resize(nl);
+  auto layer = [&](int k, const std::string& wn, const std::string& bnm, const std::string& bnp,
+                   int fin, int fout, int kind) {
+    WLayer& Lr = h->wl[k];
+    std::memset(&Lr, 0, sizeof(Lr));
+    Lr.kin = kJ * fin;
+    Lr.nout = kJ * fout;
+    Lr.fin = fin;
+    Lr.fout = fout;
+    Lr.kind = kind;
+    Lr.w_off = add(wn, Lr.kin, Lr.nout);
+    h->b_off[k] = add(bnm, 1, Lr.nout);
+    if (!bnp.empty() && h->batch_norm) {
+      h->gamma_off[k] = add(bnp + "_gamma", 1, F);
+      h->beta_off[k] = add(bnp + "_beta", 1, F);
+    }
+  };
+  layer(0, "w1", "b1", "bn0", inF, F, 0);
+  for (int l = 0; l < h->L; ++l) {
+    const std::string s = std::to_string(l);
+    layer(2 * l + 1, "w2_" + s, "b2_" + s, "bn1" + s, F, F, 1);
+    layer(2 * l + 2, "w3_" + s, "b3_" + s, "bn2" + s, F, F, 1);
+  }
+  layer(nl - 1, "w4", "b4", "", F, 3, 2);
+  h->P = off;
+
+  CHECK(dalloc(h, &h->theta, h->P));
+  CHECK(dalloc(h, &h->m, h->P));
+  CHECK(dalloc(h, &h->v, h->P));
+  CHECK(dalloc(h, &h->rg, h->P));
+  CHECK(dalloc(h, &h->gout, h->P));
+
+  // ---- block structure (joint support S[i][j] at 64-feature granularity) ----
+  auto sup = [&](int i, int j) { return h->Cmat[i * kJ + j] != 0.f; };
+  std::vector<int2> blk;
+  std::vector<int> bid(h->nslab * h->nslab, -1);
+  for (int si = 0; si < h->nslab; ++si)
+    for (int so = 0; so < h->nslab; ++so)
+      if (sup(si / h->spj, so / h->spj)) {
+        bid[si * h->nslab + so] = (int)blk.size();
+        blk.push_back(make_int2(si, so));
+      }
+  h->nblk = (int)blk.size();
+  std::vector<int> fptr(1, 0), bptr(1, 0);
+  std::vector<int2> fidx, bidx;
+  for (int so = 0; so < h->nslab; ++so) {
+    for (int si = 0; si < h->nslab; ++si)
+      if (bid[si * h->nslab + so] >= 0) fidx.push_back(make_int2(si, bid[si * h->nslab + so]));
+    fptr.push_back((int)fidx.size());
+  }
+  for (int si = 0; si < h->nslab; ++si) {
+    for (int so = 0; so < h->nslab; ++so)
+      if (bid[si * h->nslab + so] >= 0) bidx.push_back(make_int2(so, bid[si * h->nslab + so]));
+    bptr.push_back((int)bidx.size());
+  }
+  CHECK(upload(h, &h->blk, blk));
+  CHECK(upload(h, &h->fwd_ptr, fptr));
+  CHECK(upload(h, &h->bwd_ptr, bptr));
+  CHECK(upload(h, &h->fwd_idx, fidx));
+  CHECK(upload(h, &h->bwd_idx, bidx));
+  std::vector<unsigned> uml(h->nslab, 0), umo(h->nslab, 0);
+  for (int s = 0; s < h->nslab; ++s)
+    for (int u = 0; u < kJ; ++u) {
+      if (sup(u, s / h->spj)) uml[s] |= 1u << u;  // lift: input joints feeding output slab s
+      if (sup(s / h->spj, u)) umo[s] |= 1u << u;  // output: output joints fed by input slab s
+    }
+  CHECK(upload(h, &h->umask_lift, uml));
+  CHECK(upload(h, &h->umask_out, umo));
+
+  // ---- per-layer weight forms ----
+  for (int k = 0; k < nl; ++k) {
+    WLayer& Lr = h->wl[k];
+    if (Lr.kind == 1) {
+      CHECK(dalloc(h, &Lr.blk_fwd, (size_t)h->nblk * 4096));
+      CHECK(dalloc(h, &Lr.blk_bwd, (size_t)h->nblk * 4096));
+      Lr.blk = h->blk;
+      Lr.nblk = h->nblk;
+    } else if (Lr.kind == 0) {
+      CHECK(dalloc(h, &Lr.coef, (size_t)h->nslab * kJ * inF * 64));
+    } else {
+      CHECK(dalloc(h, &Lr.dense_e, (size_t)H * 51));
+      CHECK(dalloc(h, &Lr.coef, (size_t)h->nslab * 51 * 64));
+    }
+  }
+  // norms: entries [0, nl) are the weights (clip_by_norm), [nl, 2nl) the biases
+  // (only for the l2 regularisation term of the reported loss)
+  std::vector<int64_t> wo(2 * nl), ws(2 * nl);
+  std::vector<int> wk(nl), wn(nl);
+  for (int k = 0; k < nl; ++k) {
+    wo[k] = h->wl[k].w_off;
+    ws[k] = (int64_t)h->wl[k].kin * h->wl[k].nout;
+    wo[nl + k] = h->b_off[k];
+    ws[nl + k] = h->wl[k].nout;
+    wk[k] = h->wl[k].kin;
+    wn[k] = h->wl[k].nout;
+  }
+  CHECK(upload(h, &h->w_offs, wo));
+  CHECK(upload(h, &h->w_sizes, ws));
+  CHECK(upload(h, &h->w_kin, wk));
+  CHECK(upload(h, &h->w_nout, wn));
+  CHECK(upload(h, &h->Cd, h->Cmat));
+  CHECK(dalloc(h, &h->Md, kJ * kJ));
+  CHECK(dalloc(h, &h->Sd, kJ * kJ));
+  CHECK(dalloc(h, &h->denom, nl));
+  CHECK(dalloc(h, &h->lcoef, 2 * nl));
+  CHECK(dalloc(h, &h->norm_part, (size_t)2 * nl * h->norm_ppl));
+  CHECK(dalloc(h, &h->norm2, 2 * nl));
+  CHECK(dalloc(h, &h->blocksum, (size_t)nl * kJ * kJ));
+
+  // ---- Adam segments ----
+  std::vector<AdamSeg> segs;
+  std::vector<int64_t> starts;
+  int64_t blocks = 0;
+  for (const ParamSpec& ps : h->specs) {
+    AdamSeg sg{};
+    sg.off = ps.off;
+    sg.size = ps.rows * ps.cols;
+    sg.kind = 0;
+    sg.layer = -1;
+    for (int k = 0; k < nl; ++k)
+      if (h->wl[k].w_off == ps.off) {
+        sg.kind = 1;
+        sg.layer = k;
+        sg.cols = h->wl[k].nout;
+        sg.fin = h->wl[k].fin;
+        sg.fout = h->wl[k].fout;
+        sg.reg = h->reg != 0.f;
+      }
+    for (int k = 0; k < nl; ++k)
+      if (h->b_off[k] == ps.off) sg.reg = h->reg != 0.f;
+    segs.push_back(sg);
+    starts.push_back(blocks);
+    blocks += cdiv(sg.size, 1024);
+  }
+  h->nseg = (int)segs.size();
+  h->adam_blocks = blocks;
+  CHECK(upload(h, &h->segs, segs));
+  CHECK(upload(h, &h->seg_start, starts));
+
+  // ---- activations / scratch for Bmax ----
+  const int64_t B = h->Bmax;
+  CHECK(dalloc(h, &h->x, (size_t)B * kJ * inF));
+  CHECK(dalloc(h, &h->lab, (size_t)B * 51));
+  CHECK(dalloc(h, &h->out, (size_t)B * 51));
+  CHECK(dalloc(h, &h->dy, (size_t)B * 51));
+  h->Z.assign(nl - 1, nullptr);
+  for (auto& z : h->Z) CHECK(dalloc(h, &z, (size_t)B * H));
+  h->Hb.assign(h->L + 1, nullptr);
+  for (auto& hb : h->Hb) CHECK(dalloc(h, &hb, (size_t)B * H));
+  CHECK(dalloc(h, &h->DH, (size_t)B * H));
+  CHECK(dalloc(h, &h->DZ, (size_t)B * H));
+  CHECK(dalloc(h, &h->DG, (size_t)B * H));
+  h->nbn = nl - 1;
+  h->bn.resize(h->nbn);
+  std::vector<float> ones(F, 1.f), zeros(F, 0.f), ic(3 * F, 0.f);
+  for (int f = 0; f < F; ++f) ic[f] = 1.f;
+  CHECK(upload(h, &h->ident_scale, ones));
+  CHECK(upload(h, &h->ident_shift, zeros));
+  CHECK(upload(h, &h->ident_c123, ic));
+  for (auto& s : h->bn) {
+    if (h->batch_norm) {
+      CHECK(dalloc(h, &s.mean, F));
+      CHECK(dalloc(h, &s.rstd, F));
+      CHECK(dalloc(h, &s.scale, F));
+      CHECK(dalloc(h, &s.shift, F));
+    } else {
+      s.mean = h->ident_shift;
+      s.rstd = h->ident_scale;
+      s.scale = h->ident_scale;
+      s.shift = h->ident_shift;
+    }
+  }
+  CHECK(dalloc(h, &h->c123, 3 * F));
+  CHECK(dalloc(h, &h->stat_part, (size_t)cdiv(B, kLiftRows) * H));
+  CHECK(dalloc(h, &h->bpart, (size_t)cdiv(B, kEwRows) * H));
+  CHECK(dalloc(h, &h->col_part, (size_t)cdiv(B, kEwRows) * 64));
+  CHECK(dalloc(h, &h->loss_part, (size_t)cdiv(B, 64)));
+  CHECK(dalloc(h, &h->loss_sum, 4));
+  CHECK(dalloc(h, &h->acc1, 2 * F));
+  CHECK(dalloc(h, &h->acc2, 2 * F));
+  h->dw_nch_max = std::max(1, std::min(64, 8192 / std::max(1, h->nblk)));
+  CHECK(dalloc(h, &h->dw_part, (size_t)h->dw_nch_max * h->nblk * 4096));
+  h->outer_nch_max = 128;
+  CHECK(dalloc(h, &h->outer_part, (size_t)h->outer_nch_max * h->nslab * kJ * 3 * 64));
+  return LCN_OK;
+}
+
+// ---------------------------------------------------------------------------
+// step pieces
+// ---------------------------------------------------------------------------
+int allreduce(Handle* h, void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op = ncclSum) {
+  if (h->world <= 1) return LCN_OK;
+  NCCLC(ncclAllReduce(buf, buf, count, dt, op, h->comm, h->stream));
+  return LCN_OK;
+}
+
+void tstart(Handle* h, int k, hipEvent_t* pair) {
+  if (!h->timing) return;
+  hipEventCreate(&pair[0]);
+  hipEventCreate(&pair[1]);
+  hipEventRecord(pair[0], h->stream);
+  (void)k;
+}
+void tstop(Handle* h, int k, hipEvent_t* pair, double flops) {
+  if (!h->timing) return;
+  hipEventRecord(pair[1], h->stream);
+  h->timers[k].ev.push_back(pair[0]);
+  h->timers[k].ev.push_back(pair[1]);
+  h->timers[k].launches++;
+  h->timers[k].flops += flops;
+}
+
+int prep_weights(Handle* h) {
+  hipStream_t s = h->stream;
+  launch_mask(h->learnable ? h->theta + h->mask_off : nullptr, h->Cd, h->learnable, h->Md, h->Sd, s);
+  launch_wnorm(h->theta, h->w_offs, h->w_sizes, 2 * h->nl, h->norm_part, h->norm_ppl, h->norm2,
+               h->denom, h->max_norm, s);
+  for (int k = 0; k < h->nl; ++k) launch_wprep(h->theta, h->wl[k], h->Md, h->denom, k, s);
+  return LCN_OK;
+}
+
+// BN statistics of linear layer k from partials with `tile` rows per tile
+int bn_stats(Handle* h, int k, int B, int tile) {
+  if (!h->batch_norm) return LCN_OK;
+  hipStream_t s = h->stream;
+  const double count = (double)B * h->world * kJ;
+  const float* gamma = h->theta + h->gamma_off[k];
+  const float* beta = h->theta + h->beta_off[k];
+  const int nt = (int)cdiv(B, tile);
+  if (h->world == 1) {
+    launch_bn_finalize(h->stat_part, nt, tile, B, h->H, h->F, gamma, beta, h->eps, count, h->acc1,
+                       h->acc2, 0, h->bn[k], s);
+    return LCN_OK;
+  }
+  launch_bn_finalize(h->stat_part, nt, tile, B, h->H, h->F, gamma, beta, h->eps, count, h->acc1,
+                     h->acc2, 1, h->bn[k], s);
+  CHECK(allreduce(h, h->acc1, h->F, ncclDouble));
+  launch_bn_finalize(h->stat_part, nt, tile, B, h->H, h->F, gamma, beta, h->eps, count, h->acc1,
+                     h->acc2, 2, h->bn[k], s);
+  CHECK(allreduce(h, h->acc2, h->F, ncclDouble));
+  launch_bn_finalize(h->stat_part, nt, tile, B, h->H, h->F, gamma, beta, h->eps, count, h->acc1,
+                     h->acc2, 3, h->bn[k], s);
+  return LCN_OK;
+}
+
+int gemm(Handle* h, int k, int kindt, const float* X, bool pro, const BnStats* pst, float* Y,
+         const float* addsrc, bool stats, int B) {
+  const WLayer& Lr = h->wl[k];
+  GemmArgs a{};
+  a.X = X;
+  a.ldx = h->H;
+  const bool fwd = kindt == LCN_K_GEMM_FWD;
+  a.blocks = fwd ? Lr.blk_fwd : Lr.blk_bwd;
+  a.ptr = fwd ? h->fwd_ptr : h->bwd_ptr;
+  a.idx = fwd ? h->fwd_idx : h->bwd_idx;
+  a.bias = fwd ? h->theta + h->b_off[k] : nullptr;
+  a.pro_scale = pro ? pst->scale : nullptr;
+  a.pro_shift = pro ? pst->shift : nullptr;
+  a.spj_in = h->spj;
+  a.alpha = h->alpha;
+  a.Y = Y;
+  a.ldy = h->H;
+  a.addsrc = addsrc;
+  a.stat = stats ? h->stat_part : nullptr;
+  a.B = B;
+  a.n_out_slabs = h->nslab;
+  a.n_row_tiles = (int)cdiv(B, kGemmBM);
+  hipEvent_t ev[2];
+  tstart(h, kindt, ev);
+  launch_gemm_bs(a, h->stream);
+  tstop(h, kindt, ev, 2.0 * 4096.0 * 64.0 * h->nblk * B);
+  return LCN_OK;
+}
+
+int gemm_dw(Handle* h, int k, const float* A, bool pro, const BnStats* pst, const float* D, int B) {
+  GemmDwArgs a{};
+  a.A = A;
+  a.lda = h->H;
+  a.D = D;
+  a.ldd = h->H;
+  a.pro_scale = pro ? pst->scale : nullptr;
+  a.pro_shift = pro ? pst->shift : nullptr;
+  a.spj_in = h->spj;
+  a.alpha = h->alpha;
+  a.blk = h->blk;
+  a.nblk = h->nblk;
+  a.B = B;
+  const int nch = std::max(1, std::min<int>(h->dw_nch_max, (int)cdiv(B, 64)));
+  a.chunk_rows = (int)(cdiv(cdiv(B, nch), 64) * 64);
+  a.nchunks = (int)cdiv(B, a.chunk_rows);
+  a.part = h->dw_part;
+  hipEvent_t ev[2];
+  tstart(h, LCN_K_GEMM_DW, ev);
+  launch_gemm_dw(a, h->stream);
+  tstop(h, LCN_K_GEMM_DW, ev, 2.0 * 4096.0 * 64.0 * h->nblk * B);
+  launch_dw_reduce(h->dw_part, a.nchunks, h->nblk, h->blk, h->rg + h->wl[k].w_off, h->H, h->stream);
+  return LCN_OK;
+}
+
+// dz of linear layer k from the incoming gradient dh (w.r.t. the layer's
+// activation output); writes DZ, the BN parameter grads and the bias grad.
+int bn_back(Handle* h, int k, const float* dh, int B) {
+  hipStream_t s = h->stream;
+  const BnStats& st = h->bn[k];
+  const float* c123 = h->ident_c123;
+  if (h->batch_norm) {
+    const int nt = (int)cdiv(B, kEwRows);
+    const double count = (double)B * h->world * kJ;
+    launch_bnback_reduce(dh, h->Z[k], st.scale, st.shift, st.mean, st.rstd, h->F, h->alpha, 1, B,
+                         h->H, h->stat_part, s);
+    const float* gamma = h->theta + h->gamma_off[k];
+    float* dgam = h->rg + h->gamma_off[k];
+    float* dbet = h->rg + h->beta_off[k];
+    if (h->world == 1) {
+      launch_bnback_finalize(h->stat_part, nt, h->H, h->F, count, gamma, st.mean, st.rstd, h->acc1,
+                             0, dgam, dbet, h->c123, s);
+    } else {
+      launch_bnback_finalize(h->stat_part, nt, h->H, h->F, count, gamma, st.mean, st.rstd, h->acc1,
+                             1, dgam, dbet, h->c123, s);
+      CHECK(allreduce(h, h->acc1, 2 * h->F, ncclDouble));
+      launch_bnback_finalize(h->stat_part, nt, h->H, h->F, count, gamma, st.mean, st.rstd, h->acc1,
+                             2, dgam, dbet, h->c123, s);
+    }
+    c123 = h->c123;
+  }
+  launch_bnback_apply(dh, h->Z[k], st.scale, st.shift, c123, h->F, h->alpha, h->batch_norm, B, h->H,
+                      h->DZ, h->bpart, s);
+  launch_colsum(h->bpart, (int)cdiv(B, kEwRows), h->H, h->rg + h->b_off[k], s);
+  return LCN_OK;
+}
+
+int forward(Handle* h, int B, bool with_labels, bool train) {
+  hipStream_t s = h->stream;
+  const int H = h->H, nl = h->nl;
+  CHECK(prep_weights(h));
+  // lift (models_att.py:714-742)
+  ExpandArgs ea{};
+  ea.small = h->x;
+  ea.lds_small = kJ * h->inF;
+  ea.C = h->inF;
+  ea.coef = h->wl[0].coef;
+  ea.umask = h->umask_lift;
+  ea.bias = h->theta + h->b_off[0];
+  ea.out = h->Z[0];
+  ea.ldo = H;
+  ea.stat = h->batch_norm ? h->stat_part : nullptr;
+  ea.B = B;
+  ea.n_slabs = h->nslab;
+  launch_expand(ea, s);
+  CHECK(bn_stats(h, 0, B, kLiftRows));
+  launch_bn_act(h->Z[0], nullptr, h->Hb[0], h->bn[0].scale, h->bn[0].shift, h->F, h->alpha, B, H, s);
+  // two_linear blocks (models_att.py:630-705)
+  for (int l = 0; l < h->L; ++l) {
+    const int k1 = 2 * l + 1, k2 = 2 * l + 2;
+    CHECK(gemm(h, k1, LCN_K_GEMM_FWD, h->Hb[l], false, nullptr, h->Z[k1], nullptr, h->batch_norm, B));
+    CHECK(bn_stats(h, k1, B, kGemmBM));
+    CHECK(gemm(h, k2, LCN_K_GEMM_FWD, h->Z[k1], true, &h->bn[k1], h->Z[k2], nullptr, h->batch_norm,
+               B));
+    CHECK(bn_stats(h, k2, B, kGemmBM));
+    launch_bn_act(h->Z[k2], h->residual ? h->Hb[l] : nullptr, h->Hb[l + 1], h->bn[k2].scale,
+                  h->bn[k2].shift, h->F, h->alpha, B, H, s);
+  }
+  // output layer + loss (models_att.py:749-773, :356)
+  OutFwdArgs oa{};
+  oa.h = h->Hb[h->L];
+  oa.ldh = H;
+  oa.w4 = h->wl[nl - 1].dense_e;
+  oa.b4 = h->theta + h->b_off[nl - 1];
+  oa.x = h->x;
+  oa.in_f = h->inF;
+  oa.lab = with_labels ? h->lab : nullptr;
+  oa.out = h->out;
+  oa.dy = train ? h->dy : nullptr;
+  oa.loss_part = with_labels ? h->loss_part : nullptr;
+  oa.dscale = (float)(2.0 / ((double)B * h->world * 51.0));
+  oa.B = B;
+  oa.n_in_slabs = h->nslab;
+  launch_out_fwd(oa, s);
+  if (with_labels) launch_loss_finalize(h->loss_part, (int)cdiv(B, 64), h->loss_sum, s);
+  return LCN_OK;
+}
+
+int backward(Handle* h, int B) {
+  hipStream_t s = h->stream;
+  const int nl = h->nl, L = h->L;
+  // output layer: dh_L = dy . W4e^T, dW4e = h_L^T dy, db4 = sum dy
+  ExpandArgs ea{};
+  ea.small = h->dy;
+  ea.lds_small = 51;
+  ea.C = 3;
+  ea.coef = h->wl[nl - 1].coef;
+  ea.umask = h->umask_out;
+  ea.out = h->DH;
+  ea.ldo = h->H;
+  ea.B = B;
+  ea.n_slabs = h->nslab;
+  launch_expand(ea, s);
+  OuterArgs oa{};
+  oa.big = h->Hb[L];
+  oa.ldb = h->H;
+  oa.small = h->dy;
+  oa.lds_small = 51;
+  oa.C = 3;
+  oa.umask = h->umask_out;
+  oa.B = B;
+  oa.nchunks = std::max(1, std::min<int>(h->outer_nch_max, (int)cdiv(B, 64)));
+  oa.chunk_rows = (int)(cdiv(cdiv(B, oa.nchunks), 64) * 64);
+  oa.nchunks = (int)cdiv(B, oa.chunk_rows);
+  oa.n_slabs = h->nslab;
+  oa.part = h->outer_part;
+  launch_outer(oa, s);
+  launch_outer_reduce(h->outer_part, oa.nchunks, h->nslab, 3, 1, h->rg + h->wl[nl - 1].w_off, s);
+  launch_colpart(h->dy, B, 51, 51, h->col_part, s);
+  launch_colsum(h->col_part, (int)cdiv(B, kEwRows), 51, h->rg + h->b_off[nl - 1], s);
+
+  for (int l = L - 1; l >= 0; --l) {
+    const int k1 = 2 * l + 1, k2 = 2 * l + 2;
+    // DH = dh_{l+1}: gradient of the block output
+    CHECK(bn_back(h, k2, h->DH, B));                                   // DZ = dz_k2
+    CHECK(gemm_dw(h, k2, h->Z[k1], true, &h->bn[k1], h->DZ, B));       // dW_k2 = g^T dz
+    CHECK(gemm(h, k2, LCN_K_GEMM_DX, h->DZ, false, nullptr, h->DG, nullptr, false, B));  // dg
+    CHECK(bn_back(h, k1, h->DG, B));                                   // DZ = dz_k1
+    CHECK(gemm_dw(h, k1, h->Hb[l], false, nullptr, h->DZ, B));         // dW_k1 = h_l^T dz
+    CHECK(gemm(h, k1, LCN_K_GEMM_DX, h->DZ, false, nullptr, h->DH, h->residual ? h->DH : nullptr,
+               false, B));                                             // dh_l (+ residual)
+  }
+  // lift: dz0, dW1e = x^T dz0, db1
+  CHECK(bn_back(h, 0, h->DH, B));
+  OuterArgs la{};
+  la.big = h->DZ;
+  la.ldb = h->H;
+  la.small = h->x;
+  la.lds_small = kJ * h->inF;
+  la.C = h->inF;
+  la.umask = h->umask_lift;
+  la.B = B;
+  la.nchunks = oa.nchunks;
+  la.chunk_rows = oa.chunk_rows;
+  la.n_slabs = h->nslab;
+  la.part = h->outer_part;
+  launch_outer(la, s);
+  launch_outer_reduce(h->outer_part, la.nchunks, h->nslab, h->inF, 0, h->rg + h->wl[0].w_off, s);
+  return LCN_OK;
+}
+
+int finish_and_update(Handle* h, bool update, bool keep_grads) {
+  hipStream_t s = h->stream;
+  if (h->world > 1) {
+    CHECK(allreduce(h, h->rg, (size_t)h->P, ncclFloat));
+  }
+  launch_wdot(h->rg, h->theta, h->w_offs, h->w_kin, h->w_nout, h->nl, h->blocksum, s);
+  launch_maskgrad(h->blocksum, h->nl, h->Md, h->Sd, h->Cd, h->learnable, h->denom, h->norm2,
+                  h->max_norm, h->learnable ? h->rg + h->mask_off : nullptr, h->lcoef, s);
+  const float lr = h->lr0 * powf(h->decay_rate, (float)h->global_step / (float)h->decay_steps);
+  const float lr_t = lr * sqrtf(1.f - h->b2p) / (1.f - h->b1p);
+  launch_adam(h->theta, h->m, h->v, h->rg, keep_grads ? h->gout : nullptr, h->segs, h->seg_start,
+              h->nseg, h->adam_blocks, h->Md, h->lcoef, h->reg, lr_t, h->b1, h->b2, h->adam_eps,
+              update ? 1 : 0, s);
+  if (keep_grads) h->grads_valid = 1;
+  if (update) {
+    h->b1p *= h->b1;
+    h->b2p *= h->b2;
+    h->global_step += 1;
+  }
+  return LCN_OK;
+}
+
+int stage_inputs(Handle* h, const float* x, const float* lab, int64_t B, int flags) {
+  if (B <= 0 || B > h->Bmax) {
+    h->err = "batch " + std::to_string(B) + " outside [1, max_batch=" + std::to_string(h->Bmax) + "]";
+    return LCN_E_ARG;
+  }
+  const hipMemcpyKind kind = (flags & LCN_IN_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  if (x) HIPC(hipMemcpyAsync(h->x, x, (size_t)B * kJ * h->inF * 4, kind, h->stream));
+  if (lab) HIPC(hipMemcpyAsync(h->lab, lab, (size_t)B * 51 * 4, kind, h->stream));
+  h->lastB = B;
+  return LCN_OK;
+}
+
+int finish_launches(Handle* h) {
+  HIPC(hipGetLastError());
+  return LCN_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int lcn_abi_version(void) { return LCN_ABI_VERSION; }
+
+const char* lcn_last_error(void* handle) {
+  if (!handle) return g_create_error.c_str();
+  return ((Handle*)handle)->err.c_str();
+}
+
+int lcn_create(const lcn_config* c, int device, void** handle) {
+  g_create_error.clear();
+  if (!c || !handle || !c->mask_matrix) { g_create_error = "null argument"; return LCN_E_ARG; }
+  if (c->abi_version != LCN_ABI_VERSION) { g_create_error = "abi version mismatch"; return LCN_E_ARG; }
+  if (c->joints != kJ) { g_create_error = "joints must be 17 (models_att.py:512-513, params_help.py:12)"; return LCN_E_ARG; }
+  if (c->f <= 0 || c->f % kSlab) { g_create_error = "F must be a positive multiple of 64"; return LCN_E_ARG; }
+  if (c->in_f != 2 && c->in_f != 3) { g_create_error = "in_F must be 2 or 3"; return LCN_E_ARG; }
+  if (c->num_layers < 0 || c->max_batch <= 0) { g_create_error = "bad num_layers / max_batch"; return LCN_E_ARG; }
+  if (c->max_batch > (int64_t)INT32_MAX / (kJ * c->f)) { g_create_error = "max_batch too large"; return LCN_E_ARG; }
+  Handle* h = new Handle();
+  h->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    g_create_error = std::string("HIP init: ") + hipGetErrorString(e);
+    delete h;
+    return LCN_E_HIP;
+  }
+  int rc = build(h, c);
+  if (rc == LCN_OK) {
+    hipError_t e2 = hipDeviceSynchronize();
+    if (e2 != hipSuccess) { h->err = hipGetErrorString(e2); rc = LCN_E_HIP; }
+  }
+  if (rc != LCN_OK) {
+    g_create_error = h->err;
+    lcn_destroy(h);
+    return rc;
+  }
+  *handle = h;
+  return LCN_OK;
+}
+
+int lcn_destroy(void* handle) {
+  if (!handle) return LCN_OK;
+  Handle* h = (Handle*)handle;
+  hipSetDevice(h->device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->comm) ncclCommDestroy(h->comm);
+  for (auto& t : h->timers)
+    for (auto e : t.ev) hipEventDestroy(e);
+  for (void* p : h->allocs) hipFree(p);
+  for (void* p : h->user_bufs) if (p) hipFree(p);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+  return LCN_OK;
+}
+
+int64_t lcn_num_params(void* handle) { return handle ? ((Handle*)handle)->P : -1; }
+
+int lcn_param_layout(void* handle, int32_t index, char* name, int32_t cap, int64_t* offset,
+                     int64_t* rows, int64_t* cols) {
+  Handle* h = (Handle*)handle;
+  if (!h) return LCN_E_ARG;
+  if (index < 0 || index >= (int)h->specs.size()) return (int)h->specs.size();
+  const ParamSpec& p = h->specs[index];
+  if (name && cap > 0) {
+    std::strncpy(name, p.name.c_str(), cap - 1);
+    name[cap - 1] = 0;
+  }
+  if (offset) *offset = p.off;
+  if (rows) *rows = p.rows;
+  if (cols) *cols = p.cols;
+  return LCN_OK;
+}
+
+static int copy_flat(Handle* h, float* dst, const float* src, int64_t n, hipMemcpyKind kind) {
+  if (n != h->P) { h->err = "expected " + std::to_string(h->P) + " values"; return LCN_E_ARG; }
+  HIPC(hipSetDevice(h->device));
+  HIPC(hipStreamSynchronize(h->stream));
+  HIPC(hipMemcpy(dst, src, (size_t)n * 4, kind));
+  return LCN_OK;
+}
+
+int lcn_set_params(void* handle, const float* flat, int64_t n) {
+  Handle* h = (Handle*)handle;
+  if (!h || !flat) return LCN_E_ARG;
+  return copy_flat(h, h->theta, flat, n, hipMemcpyHostToDevice);
+}
+
+int lcn_get_params(void* handle, float* flat, int64_t n) {
+  Handle* h = (Handle*)handle;
+  if (!h || !flat) return LCN_E_ARG;
+  return copy_flat(h, flat, h->theta, n, hipMemcpyDeviceToHost);
+}
+
+int lcn_get_grads(void* handle, float* flat, int64_t n) {
+  Handle* h = (Handle*)handle;
+  if (!h || !flat) return LCN_E_ARG;
+  if (!h->grads_valid) { h->err = "no gradients kept (pass LCN_KEEP_GRADS to lcn_train_step)"; return LCN_E_STATE; }
+  return copy_flat(h, flat, h->gout, n, hipMemcpyDeviceToHost);
+}
+
+int lcn_set_optimizer_state(void* handle, const float* m, const float* v, int64_t n,
+                            int64_t global_step, float b1p, float b2p) {
+  Handle* h = (Handle*)handle;
+  if (!h) return LCN_E_ARG;
+  if (m) CHECK(copy_flat(h, h->m, m, n, hipMemcpyHostToDevice));
+  if (v) CHECK(copy_flat(h, h->v, v, n, hipMemcpyHostToDevice));
+  h->global_step = global_step;
+  h->b1p = b1p;
+  h->b2p = b2p;
+  return LCN_OK;
+}
+
+int lcn_get_optimizer_state(void* handle, float* m, float* v, int64_t n, int64_t* global_step,
+                            float* b1p, float* b2p) {
+  Handle* h = (Handle*)handle;
+  if (!h) return LCN_E_ARG;
+  if (m) CHECK(copy_flat(h, m, h->m, n, hipMemcpyDeviceToHost));
+  if (v) CHECK(copy_flat(h, v, h->v, n, hipMemcpyDeviceToHost));
+  if (global_step) *global_step = h->global_step;
+  if (b1p) *b1p = h->b1p;
+  if (b2p) *b2p = h->b2p;
+  return LCN_OK;
+}
+
+static int copy_out(Handle* h, float* out, int64_t B, int flags) {
+  if (!out) return LCN_OK;
+  if (flags & LCN_OUT_DEVICE) {
+    HIPC(hipMemcpyAsync(out, h->out, (size_t)B * 51 * 4, hipMemcpyDeviceToDevice, h->stream));
+  } else {
+    HIPC(hipMemcpyAsync(out, h->out, (size_t)B * 51 * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPC(hipStreamSynchronize(h->stream));
+  }
+  return LCN_OK;
+}
+
+int lcn_forward(void* handle, const float* x, float* out, int64_t B, int32_t flags) {
+  Handle* h = (Handle*)handle;
+  if (!h || !x) return LCN_E_ARG;
+  HIPC(hipSetDevice(h->device));
+  CHECK(stage_inputs(h, x, nullptr, B, flags));
+  CHECK(forward(h, (int)B, false, false));
+  CHECK(finish_launches(h));
+  CHECK(copy_out(h, out, B, flags));
+  if (!(flags & LCN_ASYNC)) HIPC(hipStreamSynchronize(h->stream));
+  return LCN_OK;
+}
+
+// mse (base_model.loss, models_att.py:356) + reg * sum(l2_loss(W), l2_loss(b))
+// when regularisation is on (:362-365); the norms are those of this step's
+// parameters (computed before the update)
+static int read_loss(Handle* h, int64_t B, float* loss) {
+  if (!loss) return LCN_OK;
+  double v = 0.0;
+  std::vector<double> n2(2 * h->nl, 0.0);
+  HIPC(hipMemcpyAsync(&v, h->loss_sum, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  if (h->reg != 0.f)
+    HIPC(hipMemcpyAsync(n2.data(), h->norm2, n2.size() * sizeof(double), hipMemcpyDeviceToHost,
+                        h->stream));
+  HIPC(hipStreamSynchronize(h->stream));
+  double l = v / ((double)B * h->world * 51.0);
+  if (h->reg != 0.f) {
+    double r = 0.0;
+    for (double x : n2) r += x / 2.0;
+    l += (double)h->reg * r;
+  }
+  *loss = (float)l;
+  return LCN_OK;
+}
+
+int lcn_forward_loss(void* handle, const float* x, const float* labels, float* out, int64_t B,
+                     int32_t flags, float* loss) {
+  Handle* h = (Handle*)handle;
+  if (!h || !x || !labels) return LCN_E_ARG;
+  HIPC(hipSetDevice(h->device));
+  CHECK(stage_inputs(h, x, labels, B, flags));
+  CHECK(forward(h, (int)B, true, false));
+  if (h->world > 1) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
+  CHECK(finish_launches(h));
+  CHECK(copy_out(h, out, B, flags));
+  CHECK(read_loss(h, B, loss));
+  if (!(flags & LCN_ASYNC)) HIPC(hipStreamSynchronize(h->stream));
+  return LCN_OK;
+}
+
+int lcn_train_step(void* handle, const float* x, const float* labels, int64_t B, int32_t flags,
+                   float* loss_out, float* lr_out) {
+  Handle* h = (Handle*)handle;
+  if (!h || !x || !labels) return LCN_E_ARG;
+  HIPC(hipSetDevice(h->device));
+  CHECK(stage_inputs(h, x, labels, B, flags));
+  const float lr = h->lr0 * powf(h->decay_rate, (float)h->global_step / (float)h->decay_steps);
+  CHECK(forward(h, (int)B, true, true));
+  if (h->world > 1) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
+  CHECK(backward(h, (int)B));
+  CHECK(finish_and_update(h, !(flags & LCN_NO_UPDATE), (flags & LCN_KEEP_GRADS) != 0));
+  CHECK(finish_launches(h));
+  if (lr_out) *lr_out = lr;
+  CHECK(read_loss(h, B, loss_out));
+  if (!(flags & LCN_ASYNC)) HIPC(hipStreamSynchronize(h->stream));
+  return LCN_OK;
+}
+
+int lcn_synchronize(void* handle) {
+  Handle* h = (Handle*)handle;
+  if (!h) return LCN_E_ARG;
+  HIPC(hipSetDevice(h->device));
+  HIPC(hipStreamSynchronize(h->stream));
+  return LCN_OK;
+}
+
+int lcn_device_buffer(void* handle, int32_t slot, int64_t bytes, void** dptr) {
+  Handle* h = (Handle*)handle;
+  if (!h || slot < 0 || slot > 64 || bytes <= 0 || !dptr) return LCN_E_ARG;
+  HIPC(hipSetDevice(h->device));
+  if ((int)h->user_bufs.size() <= slot) {
+    h->user_bufs.resize(slot + 1, nullptr);
+    h->user_bytes.resize(slot + 1, 0);
+  }
+  if (h->user_bufs[slot] && h->user_bytes[slot] >= bytes) {
+    *dptr = h->user_bufs[slot];
+    return LCN_OK;
+  }
+  if (h->user_bufs[slot]) {
+    HIPC(hipStreamSynchronize(h->stream));
+    hipFree(h->user_bufs[slot]);
+    h->user_bufs[slot] = nullptr;
+  }
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) { h->err = "hipMalloc user buffer"; return LCN_E_NOMEM; }
+  h->user_bufs[slot] = p;
+  h->user_bytes[slot] = bytes;
+  *dptr = p;
+  return LCN_OK;
+}
+
+int lcn_memcpy_h2d(void* handle, void* dst, const void* src, int64_t bytes) {
+  Handle* h = (Handle*)handle;
+  if (!h) return LCN_E_ARG;
+  HIPC(hipSetDevice(h->device));
+  HIPC(hipStreamSynchronize(h->stream));
+  HIPC(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return LCN_OK;
+}
+
+int lcn_memcpy_d2h(void* handle, void* dst, const void* src, int64_t bytes) {
+  Handle* h = (Handle*)handle;
+  if (!h) return LCN_E_ARG;
+  HIPC(hipSetDevice(h->device));
+  HIPC(hipStreamSynchronize(h->stream));
+  HIPC(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return LCN_OK;
+}
+
+int lcn_comm_unique_id(void* id_out) {
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) { g_create_error = ncclGetErrorString(r); return LCN_E_COMM; }
+  std::memcpy(id_out, &id, sizeof(id) < 128 ? sizeof(id) : 128);
+  return LCN_OK;
+}
+
+int lcn_comm_init(void* handle, const void* id_in, int32_t rank, int32_t world) {
+  Handle* h = (Handle*)handle;
+  if (!h || !id_in || world < 1 || rank < 0 || rank >= world) return LCN_E_ARG;
+  HIPC(hipSetDevice(h->device));
+  if (world == 1) { h->rank = 0; h->world = 1; return LCN_OK; }
+  ncclUniqueId id;
+  std::memcpy(&id, id_in, sizeof(id));
+  NCCLC(ncclCommInitRank(&h->comm, world, id, rank));
+  h->rank = rank;
+  h->world = world;
+  return LCN_OK;
+}
+
+int lcn_comm_allreduce_host(void* handle, double* values, int32_t count, int32_t op) {
+  Handle* h = (Handle*)handle;
+  if (!h || !values || count <= 0 || count > 2 * h->F) return LCN_E_ARG;
+  if (h->world == 1) return LCN_OK;
+  HIPC(hipSetDevice(h->device));
+  HIPC(hipStreamSynchronize(h->stream));
+  HIPC(hipMemcpy(h->acc2, values, count * sizeof(double), hipMemcpyHostToDevice));
+  NCCLC(ncclAllReduce(h->acc2, h->acc2, count, ncclDouble, op == 1 ? ncclMax : ncclSum, h->comm,
+                      h->stream));
+  HIPC(hipStreamSynchronize(h->stream));
+  HIPC(hipMemcpy(values, h->acc2, count * sizeof(double), hipMemcpyDeviceToHost));
+  return LCN_OK;
+}
+
+int lcn_set_timing(void* handle, int32_t enable) {
+  Handle* h = (Handle*)handle;
+  if (!h) return LCN_E_ARG;
+  HIPC(hipStreamSynchronize(h->stream));
+  for (auto& t : h->timers) {
+    for (auto e : t.ev) hipEventDestroy(e);
+    t = Timer();
+  }
+  h->timing = enable;
+  return LCN_OK;
+}
+
+int lcn_kernel_timing(void* handle, int32_t k, int64_t* launches, double* total_ms, double* flops) {
+  Handle* h = (Handle*)handle;
+  if (!h || k < 0 || k >= LCN_K_NUM) return LCN_E_ARG;
+  HIPC(hipStreamSynchronize(h->stream));
+  Timer& t = h->timers[k];
+  double ms = 0.0;
+  for (size_t i = 0; i + 1 < t.ev.size(); i += 2) {
+    float e = 0.f;
+    HIPC(hipEventElapsedTime(&e, t.ev[i], t.ev[i + 1]));
+    ms += e;
+  }
+  if (launches) *launches = t.launches;
+  if (total_ms) *total_ms = ms;
+  if (flops) *flops = t.flops;
+  return LCN_OK;
+}
+
+int lcn_debug_tensor(void* handle, int32_t kind, int32_t idx, float* host, int64_t n) {
+  Handle* h = (Handle*)handle;
+  if (!h || !host) return LCN_E_ARG;
+  HIPC(hipStreamSynchronize(h->stream));
+  const int64_t BH = h->lastB * h->H;
+  const float* src = nullptr;
+  int64_t cnt = 0;
+  if (kind == 0 && idx >= 0 && idx < (int)h->Z.size()) { src = h->Z[idx]; cnt = BH; }
+  else if (kind == 1 && idx >= 0 && idx < (int)h->Hb.size()) { src = h->Hb[idx]; cnt = BH; }
+  else if (kind == 2 && idx >= 0 && idx < h->nbn) {
+    if (n < 2 * h->F) return LCN_E_ARG;
+    HIPC(hipMemcpy(host, h->bn[idx].mean, h->F * 4, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(host + h->F, h->bn[idx].rstd, h->F * 4, hipMemcpyDeviceToHost));
+    return LCN_OK;
+  } else if (kind == 3) { src = h->out; cnt = h->lastB * 51; }
+  else if (kind == 4) { src = h->rg; cnt = h->P; }
+  else return LCN_E_ARG;
+  if (n < cnt) { h->err = "buffer too small"; return LCN_E_ARG; }
+  HIPC(hipMemcpy(host, src, cnt * 4, hipMemcpyDeviceToHost));
+  return LCN_OK;
+}
+
+}  // extern "C"

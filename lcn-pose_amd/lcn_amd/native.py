@@ -1,0 +1,292 @@
+"""ctypes binding of liblcn.so (the C ABI in include/lcn.h).
+
+There is no fallback: if the HIP library is missing or fails to load, every
+constructor raises ``LcnNativeError`` -- the product path never computes on
+the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("LCN_LIB", os.path.join(HERE, "liblcn.so"))
+
+LCN_ABI_VERSION = 1
+MASK_LOCALLY_CONNECTED, MASK_EXPONENTIAL = 0, 1
+IN_DEVICE, OUT_DEVICE, NO_UPDATE, KEEP_GRADS, ASYNC = 1, 2, 4, 8, 16
+K_GEMM_FWD, K_GEMM_DX, K_GEMM_DW = 0, 1, 2
+
+# every entry point include/lcn.h declares, with its ctypes signature
+_i32, _i64, _f32p, _vp = ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_float), ctypes.c_void_p
+_f64p, _i64p = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)
+
+
+class LcnConfig(ctypes.Structure):
+    _fields_ = [("abi_version", _i32), ("joints", _i32), ("in_f", _i32), ("f", _i32),
+                ("num_layers", _i32), ("mask_type", _i32), ("residual", _i32),
+                ("batch_norm", _i32), ("max_norm", _i32), ("reserved0", _i32),
+                ("bn_eps", ctypes.c_float), ("leaky_alpha", ctypes.c_float),
+                ("regularization", ctypes.c_float), ("learning_rate", ctypes.c_float),
+                ("decay_rate", ctypes.c_float), ("beta1", ctypes.c_float),
+                ("beta2", ctypes.c_float), ("adam_eps", ctypes.c_float),
+                ("decay_steps", _i64), ("max_batch", _i64), ("mask_matrix", _f32p)]
+
+
+SIGNATURES = {
+    "lcn_abi_version": ([], _i32),
+    "lcn_create": ([ctypes.POINTER(LcnConfig), _i32, ctypes.POINTER(_vp)], _i32),
+    "lcn_destroy": ([_vp], _i32),
+    "lcn_last_error": ([_vp], ctypes.c_char_p),
+    "lcn_num_params": ([_vp], _i64),
+    "lcn_param_layout": ([_vp, _i32, ctypes.c_char_p, _i32, _i64p, _i64p, _i64p], _i32),
+    "lcn_set_params": ([_vp, _f32p, _i64], _i32),
+    "lcn_get_params": ([_vp, _f32p, _i64], _i32),
+    "lcn_set_optimizer_state": ([_vp, _f32p, _f32p, _i64, _i64, ctypes.c_float, ctypes.c_float], _i32),
+    "lcn_get_optimizer_state": ([_vp, _f32p, _f32p, _i64, _i64p, _f32p, _f32p], _i32),
+    "lcn_get_grads": ([_vp, _f32p, _i64], _i32),
+    "lcn_forward": ([_vp, _vp, _vp, _i64, _i32], _i32),
+    "lcn_forward_loss": ([_vp, _vp, _vp, _vp, _i64, _i32, _f32p], _i32),
+    "lcn_train_step": ([_vp, _vp, _vp, _i64, _i32, _f32p, _f32p], _i32),
+    "lcn_synchronize": ([_vp], _i32),
+    "lcn_device_buffer": ([_vp, _i32, _i64, ctypes.POINTER(_vp)], _i32),
+    "lcn_memcpy_h2d": ([_vp, _vp, _vp, _i64], _i32),
+    "lcn_memcpy_d2h": ([_vp, _vp, _vp, _i64], _i32),
+    "lcn_comm_unique_id": ([_vp], _i32),
+    "lcn_comm_init": ([_vp, _vp, _i32, _i32], _i32),
+    "lcn_comm_allreduce_host": ([_vp, _f64p, _i32, _i32], _i32),
+    "lcn_set_timing": ([_vp, _i32], _i32),
+    "lcn_kernel_timing": ([_vp, _i32, _i64p, _f64p, _f64p], _i32),
+    "lcn_debug_tensor": ([_vp, _i32, _i32, _f32p, _i64], _i32),
+}
+
+
+class LcnNativeError(RuntimeError):
+    pass
+
+
+_LIB = None
+
+
+def load_library(path: Optional[str] = None):
+    """Load liblcn.so (raises LcnNativeError if it is missing)."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise LcnNativeError(f"liblcn.so not found at {p}: build it with "
+                             f"`python -c 'import __graft_entry__ as g; g.build()'`")
+    try:
+        lib = ctypes.CDLL(p)
+    except OSError as e:
+        raise LcnNativeError(f"cannot load {p}: {e}") from e
+    for name, (args, res) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    if lib.lcn_abi_version() != LCN_ABI_VERSION:
+        raise LcnNativeError("liblcn.so ABI version mismatch")
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def _fp(a: np.ndarray):
+    return a.ctypes.data_as(_f32p)
+
+
+def _as_f32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+class DeviceBuffer:
+    """A device allocation owned by a Network handle (slot-addressed)."""
+
+    def __init__(self, net: "Network", slot: int, nbytes: int):
+        self.net, self.slot, self.nbytes = net, slot, nbytes
+        p = _vp()
+        net._check(net.lib.lcn_device_buffer(net.h, slot, nbytes, ctypes.byref(p)))
+        self.ptr = p.value
+
+    def upload(self, arr: np.ndarray, offset_bytes: int = 0):
+        a = np.ascontiguousarray(arr)
+        assert offset_bytes + a.nbytes <= self.nbytes
+        self.net._check(self.net.lib.lcn_memcpy_h2d(self.net.h, self.ptr + offset_bytes,
+                                                    a.ctypes.data, a.nbytes))
+
+    def download(self, arr: np.ndarray, offset_bytes: int = 0):
+        assert arr.flags["C_CONTIGUOUS"] and offset_bytes + arr.nbytes <= self.nbytes
+        self.net._check(self.net.lib.lcn_memcpy_d2h(self.net.h, arr.ctypes.data,
+                                                    self.ptr + offset_bytes, arr.nbytes))
+
+
+class Network:
+    """One LCN replica on one GPU (a liblcn handle)."""
+
+    def __init__(self, *, F=64, in_F=2, num_layers=3, mask_type="locally_connected",
+                 mask_matrix: np.ndarray, residual=True, batch_norm=True, max_norm=True,
+                 regularization=0.0, learning_rate=1e-3, decay_steps=32000, decay_rate=0.96,
+                 bn_eps=1e-3, leaky_alpha=0.2, beta1=0.9, beta2=0.999, adam_eps=1e-8,
+                 max_batch=256, device=0):
+        self.lib = load_library()
+        self._mask = _as_f32(mask_matrix).reshape(17, 17).copy()
+        cfg = LcnConfig()
+        cfg.abi_version = LCN_ABI_VERSION
+        cfg.joints, cfg.in_f, cfg.f, cfg.num_layers = 17, in_F, F, num_layers
+        cfg.mask_type = MASK_LOCALLY_CONNECTED if "locally_connected" in mask_type else MASK_EXPONENTIAL
+        cfg.residual, cfg.batch_norm, cfg.max_norm = int(residual), int(batch_norm), int(max_norm)
+        cfg.bn_eps, cfg.leaky_alpha = bn_eps, leaky_alpha
+        cfg.regularization = 0.0 if regularization in (None, 0) else float(regularization)
+        cfg.learning_rate, cfg.decay_rate, cfg.decay_steps = learning_rate, decay_rate, decay_steps
+        cfg.beta1, cfg.beta2, cfg.adam_eps = beta1, beta2, adam_eps
+        cfg.max_batch = int(max_batch)
+        cfg.mask_matrix = _fp(self._mask)
+        self.cfg = cfg
+        self.F, self.in_F, self.max_batch = F, in_F, int(max_batch)
+        h = _vp()
+        rc = self.lib.lcn_create(ctypes.byref(cfg), device, ctypes.byref(h))
+        if rc != 0:
+            raise LcnNativeError(f"lcn_create failed ({rc}): {self.lib.lcn_last_error(None).decode()}")
+        self.h = h
+        self.n_params = int(self.lib.lcn_num_params(self.h))
+
+    # -- lifetime
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.lcn_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise LcnNativeError(f"liblcn error {rc}: {self.lib.lcn_last_error(self.h).decode()}")
+
+    # -- parameters
+    def param_layout(self) -> List[Tuple[str, int, Tuple[int, ...]]]:
+        out, i = [], 0
+        name = ctypes.create_string_buffer(64)
+        off, r, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        while self.lib.lcn_param_layout(self.h, i, name, 64, ctypes.byref(off), ctypes.byref(r),
+                                        ctypes.byref(c)) == 0:
+            shape = (r.value,) if r.value == 1 else (r.value, c.value)
+            if name.value.decode() == "mask":
+                shape = (17, 17)
+            out.append((name.value.decode(), off.value, shape))
+            i += 1
+        return out
+
+    def set_params(self, flat: np.ndarray):
+        f = _as_f32(flat).ravel()
+        self._check(self.lib.lcn_set_params(self.h, _fp(f), f.size))
+
+    def get_params(self) -> np.ndarray:
+        f = np.empty(self.n_params, np.float32)
+        self._check(self.lib.lcn_get_params(self.h, _fp(f), f.size))
+        return f
+
+    def get_grads(self) -> np.ndarray:
+        f = np.empty(self.n_params, np.float32)
+        self._check(self.lib.lcn_get_grads(self.h, _fp(f), f.size))
+        return f
+
+    def set_optimizer_state(self, m, v, global_step, beta1_power, beta2_power):
+        m = None if m is None else _as_f32(m).ravel()
+        v = None if v is None else _as_f32(v).ravel()
+        self._check(self.lib.lcn_set_optimizer_state(
+            self.h, None if m is None else _fp(m), None if v is None else _fp(v), self.n_params,
+            int(global_step), float(beta1_power), float(beta2_power)))
+
+    def get_optimizer_state(self):
+        m = np.empty(self.n_params, np.float32)
+        v = np.empty(self.n_params, np.float32)
+        gs, b1p, b2p = ctypes.c_int64(), ctypes.c_float(), ctypes.c_float()
+        self._check(self.lib.lcn_get_optimizer_state(self.h, _fp(m), _fp(v), self.n_params,
+                                                     ctypes.byref(gs), ctypes.byref(b1p),
+                                                     ctypes.byref(b2p)))
+        return m, v, gs.value, b1p.value, b2p.value
+
+    # -- compute
+    def forward(self, x, out: Optional[np.ndarray] = None) -> np.ndarray:
+        x = _as_f32(x)
+        B = x.shape[0]
+        if out is None:
+            out = np.empty((B, 51), np.float32)
+        self._check(self.lib.lcn_forward(self.h, x.ctypes.data, out.ctypes.data, B, 0))
+        return out
+
+    def forward_loss(self, x, labels):
+        x, labels = _as_f32(x), _as_f32(labels)
+        B = x.shape[0]
+        out = np.empty((B, 51), np.float32)
+        loss = ctypes.c_float()
+        self._check(self.lib.lcn_forward_loss(self.h, x.ctypes.data, labels.ctypes.data,
+                                              out.ctypes.data, B, 0, ctypes.byref(loss)))
+        return out, loss.value
+
+    def train_step(self, x, labels, *, update=True, keep_grads=False, want_loss=True):
+        x, labels = _as_f32(x), _as_f32(labels)
+        flags = (0 if update else NO_UPDATE) | (KEEP_GRADS if keep_grads else 0)
+        loss, lr = ctypes.c_float(), ctypes.c_float()
+        self._check(self.lib.lcn_train_step(self.h, x.ctypes.data, labels.ctypes.data, x.shape[0],
+                                            flags, ctypes.byref(loss) if want_loss else None,
+                                            ctypes.byref(lr)))
+        return (loss.value if want_loss else None), lr.value
+
+    def train_step_device(self, x_ptr: int, lab_ptr: int, batch: int, *, sync=False):
+        """One step on device-resident inputs (no host copies, no readback)."""
+        flags = IN_DEVICE | (0 if sync else ASYNC)
+        self._check(self.lib.lcn_train_step(self.h, x_ptr, lab_ptr, batch, flags, None, None))
+
+    def forward_device(self, x_ptr: int, out_ptr: int, batch: int, *, sync=False):
+        flags = IN_DEVICE | OUT_DEVICE | (0 if sync else ASYNC)
+        self._check(self.lib.lcn_forward(self.h, x_ptr, out_ptr, batch, flags))
+
+    def synchronize(self):
+        self._check(self.lib.lcn_synchronize(self.h))
+
+    def device_buffer(self, slot: int, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, slot, nbytes)
+
+    # -- data parallel
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        lib = load_library()
+        buf = ctypes.create_string_buffer(128)
+        rc = lib.lcn_comm_unique_id(buf)
+        if rc != 0:
+            raise LcnNativeError(f"lcn_comm_unique_id: {lib.lcn_last_error(None).decode()}")
+        return buf.raw
+
+    def comm_init(self, uid: bytes, rank: int, world: int):
+        buf = ctypes.create_string_buffer(uid, 128)
+        self._check(self.lib.lcn_comm_init(self.h, buf, rank, world))
+
+    def allreduce_host(self, values, op="sum") -> np.ndarray:
+        v = np.ascontiguousarray(values, dtype=np.float64).copy()
+        self._check(self.lib.lcn_comm_allreduce_host(self.h, v.ctypes.data_as(_f64p), v.size,
+                                                     1 if op == "max" else 0))
+        return v
+
+    # -- instrumentation
+    def set_timing(self, enable: bool):
+        self._check(self.lib.lcn_set_timing(self.h, int(enable)))
+
+    def kernel_timing(self, kernel: int):
+        n, ms, fl = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+        self._check(self.lib.lcn_kernel_timing(self.h, kernel, ctypes.byref(n), ctypes.byref(ms),
+                                               ctypes.byref(fl)))
+        return n.value, ms.value, fl.value
+
+    def debug_tensor(self, kind: int, idx: int, n: int) -> np.ndarray:
+        out = np.empty(n, np.float32)
+        self._check(self.lib.lcn_debug_tensor(self.h, kind, idx, _fp(out), n))
+        return out

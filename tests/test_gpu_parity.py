@@ -1,0 +1,112 @@
+"""HIP path vs the CPU oracle (runs on the MI355X box: pytest -m gpu).
+
+Tolerances (north star "1e-4"): forward outputs |d| <= 1e-4 in
+normalised units against the float64 oracle; gradients <= 1e-4 relative
+(per tensor, L2) against float64; one Adam step |d theta| <= 1e-6 absolute.
+"""
+import numpy as np
+import pytest
+
+import lcn_oracle as O
+from lcn_testutil import make_cfg, make_network, perturbed_params, rel_err, synthetic_batch
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # name, cfg kwargs, B
+    ("lc_knn3_L3", dict(F=64, L=3, knn=3), 256),
+    ("lc_knn3_B200", dict(F=64, L=3, knn=3), 200),
+    ("lc_knn1_L2", dict(F=64, L=2, knn=1), 128),
+    ("lc_knn2_L3", dict(F=64, L=3, knn=2), 300),
+    ("lc_knn5_L1", dict(F=64, L=1, knn=5), 64),
+    ("exp_L2_F128", dict(F=128, L=2, knn=2, mask="exponential"), 96),
+    ("lc_inF3", dict(F=64, L=1, knn=3, in_F=3), 160),
+    ("lc_nores", dict(F=64, L=2, knn=3, residual=False), 128),
+    ("lc_nobn", dict(F=64, L=1, knn=2, batch_norm=False), 128),
+    ("lc_noclip_reg", dict(F=64, L=1, knn=2, max_norm=False, regularization=0.01), 64),
+    ("lc_tiny_B7", dict(F=64, L=1, knn=3), 7),
+]
+
+
+def _setup(kw, B, seed=0):
+    cfg = make_cfg(**kw)
+    params = perturbed_params(cfg, seed=1 + seed)
+    x, lab = synthetic_batch(B, cfg.in_F, seed=seed)
+    net = make_network(cfg, max_batch=max(B, 8))
+    net.set_params(O.flatten(cfg, params))
+    return cfg, params, x, lab, net
+
+
+@pytest.mark.parametrize("name,kw,B", CASES, ids=[c[0] for c in CASES])
+def test_forward_matches_oracle(name, kw, B):
+    cfg, params, x, lab, net = _setup(kw, B)
+    out = net.forward(x)
+    ref64, _ = O.forward(cfg, params, x, np.float64)
+    err = np.abs(out - ref64).max()
+    assert err <= 1e-4, f"max |out - oracle64| = {err}"
+    out2, loss = net.forward_loss(x, lab)
+    np.testing.assert_array_equal(out, out2)
+    assert abs(loss - O.mse_loss(ref64, lab)) <= 1e-6 + 1e-5 * abs(loss)
+
+
+@pytest.mark.parametrize("name,kw,B", CASES, ids=[c[0] for c in CASES])
+def test_gradients_match_oracle(name, kw, B):
+    cfg, params, x, lab, net = _setup(kw, B)
+    loss, lr = net.train_step(x, lab, update=False, keep_grads=True)
+    g = O.unflatten(cfg, net.get_grads())
+    out64, cache = O.forward(cfg, params, x, np.float64)
+    ref = O.backward(cfg, params, cache, lab, np.float64)
+    assert abs(loss - (O.mse_loss(out64, lab) + O.reg_loss(cfg, params))) <= 1e-6 + 1e-5 * loss \
+        or cfg.regularization  # device loss excludes the logging-only reg term
+    bad = {}
+    for name_, _ in O.param_specs(cfg):
+        e = rel_err(g[name_], ref[name_])
+        if e > 1e-4:
+            bad[name_] = e
+    assert not bad, f"relative gradient errors above 1e-4: {bad}"
+    # params unchanged without update
+    np.testing.assert_array_equal(net.get_params(), O.flatten(cfg, params))
+
+
+def test_adam_step_matches_oracle():
+    cfg, params, x, lab, net = _setup(dict(F=64, L=2, knn=3), 256)
+    st = O.adam_init(cfg, params)
+    p_ref = {k: v.copy() for k, v in params.items()}
+    for step in range(3):
+        xs, ls = synthetic_batch(256, 2, seed=10 + step)
+        _, lr = net.train_step(xs, ls)
+        out64, cache = O.forward(cfg, p_ref, xs, np.float64)
+        g = O.backward(cfg, p_ref, cache, ls, np.float64)
+        lr_ref = O.adam_step(cfg, p_ref, {k: v.astype(np.float32) for k, v in g.items()}, st)
+        assert lr == pytest.approx(float(lr_ref), rel=1e-6)
+    got = O.unflatten(cfg, net.get_params())
+    for k in p_ref:
+        d = np.abs(got[k] - p_ref[k]).max()
+        assert d <= 5e-6, (k, d)
+    m, v, gs, b1p, b2p = net.get_optimizer_state()
+    assert gs == 3 and b1p == pytest.approx(0.9 ** 4, rel=1e-6)
+
+
+def test_train_loss_decreases():
+    cfg, params, x, lab, net = _setup(dict(F=64, L=3, knn=3), 512)
+    losses = [net.train_step(x, lab)[0] for _ in range(30)]
+    assert losses[-1] < 0.5 * losses[0], losses
+
+
+def test_duplicated_batch_gives_same_gradients():
+    """Size-independent property: BN statistics and mean-loss gradients are
+    invariant to duplicating every pose (checks the batch reductions at
+    large B without running the oracle there)."""
+    cfg = make_cfg(F=64, L=3, knn=3)
+    params = perturbed_params(cfg)
+    x, lab = synthetic_batch(8192, 2, seed=3)
+    net = make_network(cfg, max_batch=16384)
+    net.set_params(O.flatten(cfg, params))
+    net.train_step(x, lab, update=False, keep_grads=True)
+    g1 = net.get_grads()
+    net.train_step(np.concatenate([x, x]), np.concatenate([lab, lab]), update=False,
+                   keep_grads=True)
+    g2 = net.get_grads()
+    for name, off, shape in net.param_layout():
+        n = int(np.prod(shape))
+        assert rel_err(g2[off:off + n], g1[off:off + n]) < 1e-4, name
