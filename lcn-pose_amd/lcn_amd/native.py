@@ -177,9 +177,7 @@ class Network:
         off, r, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         while self.lib.lcn_param_layout(self.h, i, name, 64, ctypes.byref(off), ctypes.byref(r),
                                         ctypes.byref(c)) == 0:
-            shape = (r.value,) if r.value == 1 else (r.value, c.value)
-            if name.value.decode() == "mask":
-                shape = (17, 17)
+            shape = (c.value,) if r.value == 1 else (r.value, c.value)
             out.append((name.value.decode(), off.value, shape))
             i += 1
         return out

@@ -1,0 +1,289 @@
+"""cgcnn -- the reference's model class on the MI355X-native LCN.
+
+Drop-in for network/models_att.py of adgx/lcn-pose: same constructor
+arguments (:478-506), same fit / predict / evaluate contract (:79-286), same
+experiment/<dir_name>/{checkpoints/{final,best},summaries} layout (:431-433).
+The TensorFlow graph + Session is replaced by liblcn.so (HIP kernels for
+gfx950) through lcn_amd.native; there is no CPU compute path.
+
+Deliberate differences from the reference, all documented in DESIGN.md:
+  * resuming from a checkpoint restores the weights AND keeps them (the
+    reference re-runs the initializer after restoring, :177-180);
+  * checkpoints are written by lcn_amd.checkpoint (params + Adam slots +
+    global_step + beta powers), not by tf.train.Saver.
+"""
+from __future__ import annotations
+
+import collections
+import json
+import os
+import re
+import shutil
+import time
+
+import numpy as np
+
+from lcn_amd import checkpoint as ckpt
+from lcn_amd.init import init_flat
+from lcn_amd.native import Network
+
+ROOT_PATH = os.path.join(os.path.dirname(os.path.realpath(__file__)), "..")
+
+# models_att.py:19-36 -- the skeleton edges used for the exponential mask
+_EXP_EDGES = ((0, 1), (0, 7), (0, 4), (4, 5), (4, 7), (5, 6), (1, 7), (1, 2), (2, 3), (7, 11),
+              (7, 8), (7, 14), (11, 12), (12, 13), (14, 15), (15, 16), (8, 9), (9, 10))
+
+
+def get_exponential_matrix(verbose=True):
+    """M[i, j] = 2^-d(i, j), d = hop distance on the skeleton (models_att.py:14-69)."""
+    n = 17
+    dist = np.full((n, n), np.inf)
+    np.fill_diagonal(dist, 0)
+    for u, v in _EXP_EDGES:
+        dist[u, v] = dist[v, u] = 1
+    for k in range(n):  # Floyd-Warshall, vectorised over (i, j)
+        dist = np.minimum(dist, dist[:, k:k + 1] + dist[k:k + 1, :])
+    exp_mat = 1 / (2 ** dist)
+    if verbose:
+        print("Distances matrix:")
+        print(dist)
+        print("exp_mat:")
+        print(exp_mat)
+    return exp_mat.astype(np.float32)
+
+
+class base_model(object):
+    def __init__(self):
+        self.regularizers = []
+        self.checkpoints = "final"
+        self.writer = None
+        self._loss_ema = None
+
+    # ------------------------------------------------------------------ predict
+    def predict(self, data, labels=None, sess=None):
+        """Fixed-size batches, zero-padded last batch (models_att.py:79-132).
+
+        BatchNorm uses the statistics of each (padded) batch, as the
+        reference graph does."""
+        loss = 0
+        size = data.shape[0]
+        predictions = np.empty((size, self.out_joints * 3))
+        net = self._get_session(sess)
+        bs = self.batch_size
+        batch_data = np.zeros((bs,) + data.shape[1:], np.float32)
+        batch_labels = np.zeros((bs, self.out_joints * 3), np.float32)
+        for begin in range(0, size, bs):
+            end = min(begin + bs, size)
+            tmp = data[begin:end]
+            if not isinstance(tmp, np.ndarray):
+                tmp = tmp.toarray()  # sparse input (models_att.py:95-96)
+            batch_data[:] = 0
+            batch_data[: end - begin] = tmp
+            if labels is not None:
+                batch_labels[:] = 0
+                batch_labels[: end - begin] = labels[begin:end]
+                batch_pred, batch_loss = net.forward_loss(batch_data, batch_labels)
+                loss += batch_loss
+            else:
+                batch_pred = net.forward(batch_data)
+            predictions[begin:end] = batch_pred[: end - begin]
+        if labels is not None:
+            return predictions, loss * bs / size
+        return predictions
+
+    def evaluate(self, data, labels, sess=None):
+        t_process, t_wall = time.process_time(), time.time()
+        predictions, loss = self.predict(data, labels, sess)
+        string = "loss: {:.4e}".format(loss)
+        if sess is None:
+            string += "\ntime: {:.0f}s (wall {:.0f}s)".format(time.process_time() - t_process,
+                                                             time.time() - t_wall)
+        return string, loss
+
+    # ---------------------------------------------------------------------- fit
+    def fit(self, train_data, train_labels, val_data, val_labels, output_dir=None,
+            starting_checkpoint=None):
+        """Training loop of models_att.py:148-286 (one lcn_train_step per step)."""
+        t_process, t_wall = time.process_time(), time.time()
+        starting_step = 1
+        net = self._net
+        path = os.path.join(self._get_path("checkpoints"), "final", "model")
+        best_path = os.path.join(self._get_path("checkpoints"), "best", "model")
+        if starting_checkpoint is None:
+            shutil.rmtree(self._get_path("checkpoints"), ignore_errors=True)
+            os.makedirs(self._get_path("checkpoints"))
+            self._initialize()
+        else:
+            found = None
+            for fname in os.listdir(starting_checkpoint):
+                m = re.search(r"model-(\d+)", fname)
+                if m:
+                    found = int(m.group(1))
+            if found is None:
+                raise FileNotFoundError(f"no model-<step> checkpoint in {starting_checkpoint}")
+            starting_step = found
+            print(f"Resuming from step {starting_step}")
+            print(f"Restoring from checkpoint: {starting_checkpoint}")
+            ckpt.restore(net, ckpt.latest_checkpoint(starting_checkpoint))
+
+        losses = []
+        indices = collections.deque()
+        num_steps = int(self.num_epochs * train_data.shape[0] / self.batch_size)
+        eval_frequency = max(1, num_steps // self.num_epochs)
+        print(f"Total steps to be done to complete all the epochs: {num_steps}")
+        min_loss = 10000
+        training_error, validation_error = [], []
+        loss_average = float("nan")
+        for step in range(starting_step, num_steps + 1):
+            if len(indices) < self.batch_size:
+                indices.extend(np.random.permutation(train_data.shape[0]))
+            idx = [indices.popleft() for _ in range(self.batch_size)]
+            batch_data, batch_labels = train_data[idx, ...], train_labels[idx, ...]
+            loss, learning_rate = net.train_step(batch_data, batch_labels)
+            loss_average = self._update_loss_average(loss)
+
+            if step % eval_frequency == 0:
+                epoch = step * self.batch_size / train_data.shape[0]
+                print("step {} / {} (epoch {:.2f} / {}):".format(step, num_steps, epoch,
+                                                                 self.num_epochs))
+                print("  learning_rate = {:.2e}, loss_average = {:.4e}".format(learning_rate,
+                                                                               loss_average))
+                training_error.append([time.time(), step, loss_average])
+                string, loss = self.evaluate(val_data, val_labels, net)
+                losses.append(loss)
+                print("validation {}".format(string))
+                print("time: {:.0f}s (wall {:.0f}s)".format(time.process_time() - t_process,
+                                                           time.time() - t_wall))
+                validation_error.append([0, step, loss])
+                self._write_summary(step, learning_rate, loss_average, loss)
+                ckpt.save(net, path, step, self._ckpt_meta())
+                if loss < min_loss:
+                    min_loss = loss
+                    ckpt.save(net, best_path, step, self._ckpt_meta())
+
+        print("validation loss: trough = {:.4f}, mean = {:.2f}".format(
+            min_loss, np.mean(losses[-10:]) if losses else float("nan")))
+        t_step = (time.time() - t_wall) / max(num_steps, 1)
+        if output_dir is not None:
+            os.makedirs(output_dir, exist_ok=True)
+            with open(output_dir + "/training_error.json", "w") as f:
+                f.write(json.dumps([training_error], indent=4))
+            with open(output_dir + "/validation_error.json", "w") as f:
+                f.write(json.dumps([validation_error], indent=4))
+        if training_error:
+            print("Final training error: ", training_error[-1])
+            print("Final validation error: ", validation_error[-1])
+        return losses, t_step
+
+    # ----------------------------------------------------------------- helpers
+    def _update_loss_average(self, loss):
+        """tf.train.ExponentialMovingAverage(0.9) of a tensor: zero-debiased
+        (models_att.py:370-379)."""
+        if self._loss_ema is None:
+            self._loss_ema = [0.0, 0]
+        biased, n = self._loss_ema
+        biased = 0.9 * biased + 0.1 * float(loss)
+        n += 1
+        self._loss_ema = [biased, n]
+        return biased / (1 - 0.9 ** n)
+
+    def _write_summary(self, step, lr, loss_average, val_loss):
+        d = self._get_path("summaries")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "scalars.jsonl"), "a") as f:
+            f.write(json.dumps({"step": step, "learning_rate": lr, "loss/avg/total": loss_average,
+                                "validation/loss": val_loss}) + "\n")
+
+    def get_var(self, name):
+        net = self._get_session()
+        for n, off, shape in net.param_layout():
+            if n == name:
+                return net.get_params()[off:off + int(np.prod(shape))].reshape(shape)
+        raise KeyError(name)
+
+    def _get_path(self, folder):
+        path = os.path.dirname(os.path.realpath(__file__))
+        return os.path.join(path, "..", "experiment", self.dir_name, folder)
+
+    def _get_session(self, sess=None):
+        """sess=None: restore the latest <checkpoints> checkpoint (models_att.py:445-463)."""
+        if sess is not None:
+            return sess
+        print(self._get_path("checkpoints"))
+        filename = ckpt.latest_checkpoint(os.path.join(self._get_path("checkpoints"), self.checkpoints))
+        print("restore from %s" % filename)
+        if filename is None:
+            raise FileNotFoundError("no checkpoint under " + self._get_path("checkpoints"))
+        ckpt.restore(self._net, filename)
+        return self._net
+
+
+class cgcnn(base_model):
+    def __init__(self, F=64, mask_type="locally_connected", init_type="ones", neighbour_matrix=None,
+                 in_joints=17, out_joints=17, in_F=2, num_layers=2, residual=True, batch_norm=True,
+                 max_norm=True, num_epochs=200, learning_rate=0.001, decay_type="exp",
+                 decay_params=None, regularization=0.0, dropout=0, batch_size=200,
+                 eval_frequency=200, dir_name="", checkpoints="final", is_training=True, knn=1):
+        super().__init__()
+        self.F = F
+        self.mask_type = mask_type
+        self.init_type = init_type
+        assert neighbour_matrix.shape[0] == neighbour_matrix.shape[1]
+        assert neighbour_matrix.shape[0] == in_joints
+        self.neighbour_matrix = neighbour_matrix
+        self.in_joints, self.out_joints = in_joints, out_joints
+        self.num_layers = num_layers
+        self.residual, self.batch_norm, self.max_norm = residual, batch_norm, max_norm
+        self.num_epochs, self.learning_rate = num_epochs, learning_rate
+        self.decay_type, self.decay_params = decay_type, decay_params
+        self.regularization, self.dropout = regularization, dropout
+        self.batch_size, self.eval_frequency = batch_size, eval_frequency
+        self.dir_name = dir_name
+        self.checkpoints = checkpoints
+        self.in_F = in_F
+        self.is_training = is_training
+        self.knn = knn
+        self.build_graph(in_joints, in_F)
+
+    def build_graph(self, M_0, in_F):
+        self.initialize_mask()
+        if self.decay_type != "exp":
+            raise AssertionError("not implemented lr decay types!")
+        if self.dropout not in (0, None, 0.0):
+            raise NotImplementedError("dropout > 0 is not implemented on the MI355X path yet")
+        dp = self.decay_params or {"decay_steps": 32000, "decay_rate": 0.96}
+        self._net = Network(F=self.F, in_F=in_F, num_layers=self.num_layers,
+                            mask_type=self.mask_type, mask_matrix=self._mask_matrix,
+                            residual=self.residual, batch_norm=self.batch_norm,
+                            max_norm=self.max_norm, regularization=self.regularization,
+                            learning_rate=self.learning_rate, decay_steps=dp["decay_steps"],
+                            decay_rate=dp["decay_rate"], max_batch=self.batch_size,
+                            device=int(os.environ.get("LOCAL_RANK", "0")))
+        self._initialize()
+        if os.path.exists(self._get_path("summaries")):
+            shutil.rmtree(self._get_path("summaries"))
+
+    def initialize_mask(self):
+        """models_att.py:534-574: LC mask = softmax(V, 0) (.) 1[N^T != 0] with V
+        trainable and initialised to N^T; exponential mask = constant."""
+        if "locally_connected" in self.mask_type:
+            assert self.neighbour_matrix is not None
+            L = np.asarray(self.neighbour_matrix).T
+            assert L.shape == (self.in_joints, self.in_joints)
+            if self.init_type != "same":
+                raise ValueError("Unknown init_type: {}".format(self.init_type))
+            self._mask_matrix = (L != 0).astype(np.float32)
+        if "exponential" in self.mask_type:
+            self._mask_matrix = get_exponential_matrix()
+
+    def _initialize(self):
+        flat = init_flat(self._net.param_layout(), self._net.n_params, self.neighbour_matrix)
+        self._net.set_params(flat)
+        n = self._net.n_params
+        self._net.set_optimizer_state(np.zeros(n, np.float32), np.zeros(n, np.float32), 0, 0.9, 0.999)
+        self._loss_ema = None
+
+    def _ckpt_meta(self):
+        return {"F": self.F, "mask_type": self.mask_type, "num_layers": self.num_layers,
+                "in_F": self.in_F, "knn": self.knn, "residual": self.residual,
+                "batch_norm": self.batch_norm, "max_norm": self.max_norm}

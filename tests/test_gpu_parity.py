@@ -46,7 +46,9 @@ def test_forward_matches_oracle(name, kw, B):
     assert err <= 1e-4, f"max |out - oracle64| = {err}"
     out2, loss = net.forward_loss(x, lab)
     np.testing.assert_array_equal(out, out2)
-    assert abs(loss - O.mse_loss(ref64, lab)) <= 1e-6 + 1e-5 * abs(loss)
+    # op_loss = mse + reg * sum l2_loss(W, b)  (models_att.py:356-365)
+    expect = O.mse_loss(ref64, lab) + O.reg_loss(cfg, params)
+    assert abs(loss - expect) <= 1e-6 + 1e-5 * abs(expect)
 
 
 @pytest.mark.parametrize("name,kw,B", CASES, ids=[c[0] for c in CASES])
@@ -56,8 +58,8 @@ def test_gradients_match_oracle(name, kw, B):
     g = O.unflatten(cfg, net.get_grads())
     out64, cache = O.forward(cfg, params, x, np.float64)
     ref = O.backward(cfg, params, cache, lab, np.float64)
-    assert abs(loss - (O.mse_loss(out64, lab) + O.reg_loss(cfg, params))) <= 1e-6 + 1e-5 * loss \
-        or cfg.regularization  # device loss excludes the logging-only reg term
+    expect = O.mse_loss(out64, lab) + O.reg_loss(cfg, params)
+    assert abs(loss - expect) <= 1e-6 + 1e-5 * abs(expect)
     bad = {}
     for name_, _ in O.param_specs(cfg):
         e = rel_err(g[name_], ref[name_])
