@@ -473,7 +473,7 @@ int gemm(Handle* h, int k, int kindt, const float* X, bool pro, const BnStats* p
   hipEvent_t ev[2];
   tstart(h, kindt, ev);
   launch_gemm_bs(a, h->stream);
-  tstop(h, kindt, ev, 2.0 * 4096.0 * 64.0 * h->nblk * B);
+  tstop(h, kindt, ev, 2.0 * 4096.0 * h->nblk * B);  // 2*64*64 FLOP per block per row
   return LCN_OK;
 }
 
@@ -497,7 +497,7 @@ int gemm_dw(Handle* h, int k, const float* A, bool pro, const BnStats* pst, cons
   hipEvent_t ev[2];
   tstart(h, LCN_K_GEMM_DW, ev);
   launch_gemm_dw(a, h->stream);
-  tstop(h, LCN_K_GEMM_DW, ev, 2.0 * 4096.0 * 64.0 * h->nblk * B);
+  tstop(h, LCN_K_GEMM_DW, ev, 2.0 * 4096.0 * h->nblk * B);  // 2*64*64 FLOP per block per row
   launch_dw_reduce(h->dw_part, a.nchunks, h->nblk, h->blk, h->rg + h->wl[k].w_off, h->H, h->stream);
   return LCN_OK;
 }
