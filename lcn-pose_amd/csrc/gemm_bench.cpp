@@ -1,0 +1,195 @@
+// Stand-alone timing of the block-sparse GEMM kernels at the cfg3 shape
+// (B = 65 536, F = 64, knn = 3: 175 blocks), random data, HIP events.
+// Build: make gemm_bench ; run: ./gemm_bench [B] [iters]
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "lcn_internal.h"
+
+using namespace lcn;
+
+#define CK(x)                                                                     \
+  do {                                                                            \
+    hipError_t e = (x);                                                           \
+    if (e != hipSuccess) {                                                        \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+      std::exit(1);                                                               \
+    }                                                                             \
+  } while (0)
+
+static const int kNbr[17][7] = {{1, 4, 7, -1}, {0, 7, 2, -1}, {1, 3, -1}, {2, -1}, {0, 7, 5, -1},
+                                {4, 6, -1}, {5, -1}, {1, 0, 4, 14, 8, 11, -1}, {7, 9, 11, 14, -1},
+                                {8, 10, -1}, {9, -1}, {8, 7, 12, -1}, {11, 13, -1}, {12, -1},
+                                {8, 7, 15, -1}, {14, 16, -1}, {15, -1}};
+
+template <typename T>
+T* dev(const std::vector<T>& v) {
+  T* p;
+  CK(hipMalloc(&p, v.size() * sizeof(T)));
+  CK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return p;
+}
+
+int main(int argc, char** argv) {
+  const int B = argc > 1 ? std::atoi(argv[1]) : 65536;
+  const int iters = argc > 2 ? std::atoi(argv[2]) : 20;
+  const int knn = argc > 3 ? std::atoi(argv[3]) : 3;
+  const int J = 17, F = 64, H = J * F;
+  // structure N = (A+I)^knn != 0
+  std::vector<int> A(J * J, 0);
+  for (int i = 0; i < J; ++i) {
+    A[i * J + i] = 1;
+    for (int k = 0; kNbr[i][k] >= 0; ++k) A[i * J + kNbr[i][k]] = 1;
+  }
+  std::vector<int> N = A;
+  for (int p = 1; p < knn; ++p) {
+    std::vector<int> T(J * J, 0);
+    for (int i = 0; i < J; ++i)
+      for (int j = 0; j < J; ++j)
+        for (int k = 0; k < J; ++k) T[i * J + j] |= N[i * J + k] && A[k * J + j];
+    N = T;
+  }
+  std::vector<int2> blk;
+  std::vector<int> bid(J * J, -1);
+  for (int i = 0; i < J; ++i)
+    for (int j = 0; j < J; ++j)
+      if (N[j * J + i]) { bid[i * J + j] = (int)blk.size(); blk.push_back(make_int2(i, j)); }
+  std::vector<int> fptr(1, 0), bptr(1, 0);
+  std::vector<int2> fidx, bidx;
+  for (int so = 0; so < J; ++so) {
+    for (int si = 0; si < J; ++si)
+      if (bid[si * J + so] >= 0) fidx.push_back(make_int2(si, bid[si * J + so]));
+    fptr.push_back((int)fidx.size());
+  }
+  for (int si = 0; si < J; ++si) {
+    for (int so = 0; so < J; ++so)
+      if (bid[si * J + so] >= 0) bidx.push_back(make_int2(so, bid[si * J + so]));
+    bptr.push_back((int)bidx.size());
+  }
+  const int nblk = (int)blk.size();
+  std::printf("B=%d knn=%d nblk=%d\n", B, knn, nblk);
+
+  std::mt19937 rng(1);
+  std::uniform_real_distribution<float> U(-1.f, 1.f);
+  std::vector<float> hx((size_t)B * H), hw((size_t)nblk * 4096), hb(H), hs(F), hh(F);
+  for (auto& v : hx) v = U(rng);
+  for (auto& v : hw) v = U(rng) * 0.05f;
+  for (auto& v : hb) v = U(rng);
+  for (int f = 0; f < F; ++f) { hs[f] = 1.f + 0.1f * U(rng); hh[f] = 0.1f * U(rng); }
+  float* X = dev(hx);
+  float* X2 = dev(hx);
+  float* W = dev(hw);
+  float* bias = dev(hb);
+  float* sc = dev(hs);
+  float* sh = dev(hh);
+  int2* dblk = dev(blk);
+  int* dfp = dev(fptr);
+  int* dbp = dev(bptr);
+  int2* dfi = dev(fidx);
+  int2* dbi = dev(bidx);
+  float* Y;
+  CK(hipMalloc(&Y, (size_t)B * H * 4));
+  float2* stat;
+  CK(hipMalloc(&stat, (size_t)(B / 64 + 1) * H * 8));
+  const int nch = std::max(1, std::min(64, 8192 / nblk));
+  float* part;
+  CK(hipMalloc(&part, (size_t)nch * nblk * 4096 * 4));
+  float* dW;
+  CK(hipMalloc(&dW, (size_t)H * H * 4));
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const double flop = 2.0 * 4096.0 * nblk * B;
+
+  auto mk = [&](bool fwd, bool pro, bool stats, int variant) {
+    GemmArgs a{};
+    a.X = X;
+    a.ldx = H;
+    a.blocks = W;
+    a.ptr = fwd ? dfp : dbp;
+    a.idx = fwd ? dfi : dbi;
+    a.bias = fwd ? bias : nullptr;
+    a.pro_scale = pro ? sc : nullptr;
+    a.pro_shift = pro ? sh : nullptr;
+    a.spj_in = 1;
+    a.alpha = 0.2f;
+    a.Y = Y;
+    a.ldy = H;
+    a.addsrc = fwd ? nullptr : Y;
+    a.stat = stats ? stat : nullptr;
+    a.B = B;
+    a.n_out_slabs = J;
+    a.variant = variant;
+    a.n_row_tiles = (B + gemm_bs_rows(variant) - 1) / gemm_bs_rows(variant);
+    return a;
+  };
+  GemmDwArgs d{};
+  d.A = X;
+  d.lda = H;
+  d.D = X2;
+  d.ldd = H;
+  d.spj_in = 1;
+  d.alpha = 0.2f;
+  d.blk = dblk;
+  d.nblk = nblk;
+  d.B = B;
+  d.chunk_rows = ((B + nch - 1) / nch + 63) / 64 * 64;
+  d.nchunks = (B + d.chunk_rows - 1) / d.chunk_rows;
+  d.part = part;
+
+  struct Case { const char* name; int kind; bool pro; bool stats; int variant; };
+  std::vector<Case> cases;
+  const int nvar = argc > 4 ? std::atoi(argv[4]) : 3;
+  for (int v = 0; v < nvar; ++v) {
+    cases.push_back({"fwd raw +stats", 0, false, true, v});
+    cases.push_back({"fwd bnact +stats", 0, true, true, v});
+    cases.push_back({"dx +residual", 1, false, false, v});
+  }
+  cases.push_back({"dw raw", 2, false, false, 0});
+  cases.push_back({"dw bnact", 2, true, false, 0});
+  const int rounds = 3;
+  for (int r = 0; r < rounds; ++r) {
+    for (const Case& c : cases) {
+      auto run = [&]() {
+        if (c.kind == 2) {
+          d.pro_scale = c.pro ? sc : nullptr;
+          d.pro_shift = c.pro ? sh : nullptr;
+          launch_gemm_dw(d, s);
+          launch_dw_reduce(part, d.nchunks, nblk, dblk, dW, H, s);
+        } else {
+          launch_gemm_bs(mk(c.kind == 0, c.pro, c.stats, c.variant), s);
+        }
+      };
+      run();
+      CK(hipStreamSynchronize(s));
+      CK(hipEventRecord(e0, s));
+      for (int it = 0; it < iters; ++it) run();
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= iters;
+      std::printf("round %d v%d %-18s %8.1f us  %6.1f TFLOP/s  (%.1f%% of 157.3)\n", r, c.variant, c.name,
+                  ms * 1e3, flop / (ms * 1e-3) / 1e12, 100.0 * flop / (ms * 1e-3) / 1e12 / 157.3);
+      if (r == 0 && c.kind == 0) {  // cross-check every variant's forward output against v0
+        static std::vector<float> ref[2];
+        std::vector<float> got((size_t)B * H);
+        CK(hipMemcpy(got.data(), Y, got.size() * 4, hipMemcpyDeviceToHost));
+        std::vector<float>& rf = ref[c.pro ? 1 : 0];
+        if (rf.empty()) rf = got;
+        double md = 0;
+        for (size_t i = 0; i < got.size(); ++i) md = std::max(md, (double)std::fabs(got[i] - rf[i]));
+        std::printf("   max |Y - Y_v0| = %.3e\n", md);
+      }
+    }
+  }
+  CK(hipGetLastError());
+  return 0;
+}

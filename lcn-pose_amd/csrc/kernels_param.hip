@@ -100,31 +100,40 @@ __global__ __launch_bounds__(256) void wprep_hidden_kernel(const float* __restri
   }
 }
 
-// lift: coef[s][u][c][f] = W_e[u*C + c][s*64 + f]
-__global__ void wprep_lift_kernel(const float* __restrict__ W, int C, int nslab, int spj,
-                                  const float* __restrict__ M, const float* __restrict__ denom,
-                                  int layer, float* __restrict__ coef) {
-  const int total = nslab * kJ * C * 64;
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= total) return;
-  const int f = e & 63, uc = (e >> 6) % (kJ * C), s = (e >> 6) / (kJ * C);
-  const int u = uc / C;
-  const float m = M[u * kJ + s / spj];
-  coef[e] = (W[(size_t)uc * (nslab * 64) + s * 64 + f] / denom[layer]) * m;
+// lift (K = 17*C padded to 64): blk[so][f][k] = W_e[k][so*64 + f], zero for k >= 17*C
+__global__ __launch_bounds__(256) void wprep_lift_kernel(const float* __restrict__ W, int C,
+                                                         int nslab, int spj,
+                                                         const float* __restrict__ M,
+                                                         const float* __restrict__ denom, int layer,
+                                                         float* __restrict__ blk) {
+  const int so = blockIdx.x, ld = nslab * 64;
+  const float dn = denom[layer];
+  for (int e = threadIdx.x; e < 4096; e += 256) {
+    const int f = e >> 6, k = e & 63;
+    float v = 0.f;
+    if (k < kJ * C) v = (W[(size_t)k * ld + so * 64 + f] / dn) * M[(k / C) * kJ + so / spj];
+    blk[(size_t)so * 4096 + e] = v;
+  }
 }
 
-// output: dense W_e [H][3J] and the dX expand coefficients coef[s][u][c][f] = W_e[s*64+f][u*3+c]
-__global__ void wprep_out_kernel(const float* __restrict__ W, int F, int nslab,
-                                 const float* __restrict__ M, const float* __restrict__ denom,
-                                 int layer, float* __restrict__ dense, float* __restrict__ coef) {
-  const int H = nslab * 64, N = kJ * 3;
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= H * N) return;
-  const int r = e / N, c = e - r * N;
-  const float v = (W[e] / denom[layer]) * M[(r / F) * kJ + c / 3];
-  dense[e] = v;
-  const int s = r >> 6, f = r & 63;
-  coef[((size_t)s * N + c) * 64 + f] = v;
+// output (N = 51 padded to 64): fwd[si][c'][p] and bwd[si][p][c'] = W_e[si*64+p][c'],
+// zero for c' >= 51
+__global__ __launch_bounds__(256) void wprep_out_kernel(const float* __restrict__ W, int F,
+                                                        const float* __restrict__ M,
+                                                        const float* __restrict__ denom, int layer,
+                                                        float* __restrict__ fwd,
+                                                        float* __restrict__ bwd) {
+  constexpr int N = kJ * 3;
+  const int si = blockIdx.x;
+  const float dn = denom[layer];
+  for (int e = threadIdx.x; e < 4096; e += 256) {
+    const int p = e >> 6, c = e & 63;  // bwd layout: coalesced W reads along c
+    const int r = si * 64 + p;
+    float v = 0.f;
+    if (c < N) v = (W[(size_t)r * N + c] / dn) * M[(r / F) * kJ + c / 3];
+    bwd[(size_t)si * 4096 + e] = v;
+    fwd[(size_t)si * 4096 + c * 64 + p] = v;
+  }
 }
 
 void launch_wprep(const float* params, const WLayer& L, const float* M, const float* denom,
@@ -136,14 +145,12 @@ void launch_wprep(const float* params, const WLayer& L, const float* M, const fl
                        denom, layer, L.blk_fwd, L.blk_bwd);
   } else if (L.kind == 0) {
     const int nslab = L.nout / 64, spj = L.fout / 64;
-    const int total = nslab * kJ * L.fin * 64;
-    hipLaunchKernelGGL(wprep_lift_kernel, dim3((total + 255) / 256), dim3(256), 0, s, W, L.fin,
-                       nslab, spj, M, denom, layer, L.coef);
+    hipLaunchKernelGGL(wprep_lift_kernel, dim3(nslab), dim3(256), 0, s, W, L.fin, nslab, spj, M,
+                       denom, layer, L.blk_fwd);
   } else {
     const int nslab = L.kin / 64;
-    const int total = L.kin * L.nout;
-    hipLaunchKernelGGL(wprep_out_kernel, dim3((total + 255) / 256), dim3(256), 0, s, W, L.fin,
-                       nslab, M, denom, layer, L.dense_e, L.coef);
+    hipLaunchKernelGGL(wprep_out_kernel, dim3(nslab), dim3(256), 0, s, W, L.fin, M, denom, layer,
+                       L.blk_fwd, L.blk_bwd);
   }
 }
 

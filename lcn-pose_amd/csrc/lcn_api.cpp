@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -70,7 +71,8 @@ struct Handle {
   int nblk = 0;
   int *fwd_ptr = nullptr, *bwd_ptr = nullptr;
   int2 *fwd_idx = nullptr, *bwd_idx = nullptr, *blk = nullptr;
-  unsigned *umask_lift = nullptr, *umask_out = nullptr;
+  int *thin_ptr = nullptr, *out_ptr = nullptr;                  // thin layers (padded slab)
+  int2 *thin_idx = nullptr, *out_idx = nullptr, *lift_blk = nullptr, *out_blk = nullptr;
 
   // mask / norms
   float *Md = nullptr, *Sd = nullptr, *Cd = nullptr, *denom = nullptr, *lcoef = nullptr;
@@ -80,16 +82,17 @@ struct Handle {
   int norm_ppl = 64;
 
   // activations
-  float *x = nullptr, *lab = nullptr, *out = nullptr, *dy = nullptr;
+  // x / y / dy of the thin layers are padded to 64 columns (pads stay zero)
+  float *x = nullptr, *lab = nullptr, *out = nullptr, *dy = nullptr, *yout = nullptr;
   std::vector<float*> Z, Hb;
   float *DH = nullptr, *DZ = nullptr, *DG = nullptr;
   std::vector<BnStats> bn;
   float *ident_scale = nullptr, *ident_shift = nullptr, *ident_c123 = nullptr;
   float* c123 = nullptr;
   float2* stat_part = nullptr;
-  float *bpart = nullptr, *dw_part = nullptr, *outer_part = nullptr, *col_part = nullptr;
+  float *bpart = nullptr, *dw_part = nullptr, *col_part = nullptr;
   double *loss_part = nullptr, *loss_sum = nullptr, *acc1 = nullptr, *acc2 = nullptr;
-  int dw_nch_max = 1, outer_nch_max = 1;
+  int loss_grid = 1;
 
   // Adam segments
   AdamSeg* segs = nullptr;
@@ -107,6 +110,9 @@ struct Handle {
   // communication
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
+
+  // block-sparse GEMM variant (kernels_gemm.hip); LCN_GEMM_VARIANT overrides
+  int gemm_variant = 0;
 
   // instrumentation
   int timing = 0;
@@ -162,6 +168,9 @@ int upload(Handle* h, T** p, const std::vector<T>& src) {
 
 int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// batch chunks of the weight-gradient GEMM: ~8k workgroups in total, <= 64 chunks
+int dw_chunks(int nblk) { return std::max(1, std::min(64, 8192 / std::max(1, nblk))); }
+
 // ---------------------------------------------------------------------------
 // construction
 // ---------------------------------------------------------------------------
@@ -189,6 +198,7 @@ int build(Handle* h, const lcn_config* c) {
   h->b1p = h->b1;
   h->b2p = h->b2;
   h->Bmax = c->max_batch;
+  if (const char* gv = std::getenv("LCN_GEMM_VARIANT")) h->gemm_variant = std::atoi(gv);
   h->Cmat.assign(c->mask_matrix, c->mask_matrix + kJ * kJ);
   const int H = h->H, F = h->F, inF = h->inF, nl = h->nl;
 
@@ -263,14 +273,30 @@ int build(Handle* h, const lcn_config* c) {
   CHECK(upload(h, &h->bwd_ptr, bptr));
   CHECK(upload(h, &h->fwd_idx, fidx));
   CHECK(upload(h, &h->bwd_idx, bidx));
-  std::vector<unsigned> uml(h->nslab, 0), umo(h->nslab, 0);
-  for (int s = 0; s < h->nslab; ++s)
-    for (int u = 0; u < kJ; ++u) {
-      if (sup(u, s / h->spj)) uml[s] |= 1u << u;  // lift: input joints feeding output slab s
-      if (sup(s / h->spj, u)) umo[s] |= 1u << u;  // output: output joints fed by input slab s
+  for (int so = 0; so < h->nslab; ++so)
+    if (fptr[so + 1] == fptr[so]) {
+      h->err = "output joint " + std::to_string(so / h->spj) + " has no input joint in the mask";
+      return LCN_E_ARG;
     }
-  CHECK(upload(h, &h->umask_lift, uml));
-  CHECK(upload(h, &h->umask_out, umo));
+  // Thin layers as one padded 64-wide slab on the narrow side:
+  //   lift:  input slab 0 (x padded to 64) -> every output slab so, block so
+  //   out:   every input slab si -> output slab 0 (51 of 64 columns), block si
+  //   out^T: input slab 0 (dy padded) -> every output slab so, block so
+  std::vector<int> tptr, optr{0, h->nslab};
+  std::vector<int2> tidx, oidx, lblk, oblk;
+  for (int s = 0; s <= h->nslab; ++s) tptr.push_back(s);
+  for (int s = 0; s < h->nslab; ++s) {
+    tidx.push_back(make_int2(0, s));
+    oidx.push_back(make_int2(s, s));
+    lblk.push_back(make_int2(0, s));
+    oblk.push_back(make_int2(s, 0));
+  }
+  CHECK(upload(h, &h->thin_ptr, tptr));
+  CHECK(upload(h, &h->thin_idx, tidx));
+  CHECK(upload(h, &h->out_ptr, optr));
+  CHECK(upload(h, &h->out_idx, oidx));
+  CHECK(upload(h, &h->lift_blk, lblk));
+  CHECK(upload(h, &h->out_blk, oblk));
 
   // ---- per-layer weight forms ----
   for (int k = 0; k < nl; ++k) {
@@ -281,10 +307,10 @@ int build(Handle* h, const lcn_config* c) {
       Lr.blk = h->blk;
       Lr.nblk = h->nblk;
     } else if (Lr.kind == 0) {
-      CHECK(dalloc(h, &Lr.coef, (size_t)h->nslab * kJ * inF * 64));
+      CHECK(dalloc(h, &Lr.blk_fwd, (size_t)h->nslab * 4096));
     } else {
-      CHECK(dalloc(h, &Lr.dense_e, (size_t)H * 51));
-      CHECK(dalloc(h, &Lr.coef, (size_t)h->nslab * 51 * 64));
+      CHECK(dalloc(h, &Lr.blk_fwd, (size_t)h->nslab * 4096));
+      CHECK(dalloc(h, &Lr.blk_bwd, (size_t)h->nslab * 4096));
     }
   }
   // norms: entries [0, nl) are the weights (clip_by_norm), [nl, 2nl) the biases
@@ -344,10 +370,11 @@ int build(Handle* h, const lcn_config* c) {
 
   // ---- activations / scratch for Bmax ----
   const int64_t B = h->Bmax;
-  CHECK(dalloc(h, &h->x, (size_t)B * kJ * inF));
+  CHECK(dalloc(h, &h->x, (size_t)B * 64));
   CHECK(dalloc(h, &h->lab, (size_t)B * 51));
   CHECK(dalloc(h, &h->out, (size_t)B * 51));
-  CHECK(dalloc(h, &h->dy, (size_t)B * 51));
+  CHECK(dalloc(h, &h->dy, (size_t)B * 64));
+  CHECK(dalloc(h, &h->yout, (size_t)B * 64));
   h->Z.assign(nl - 1, nullptr);
   for (auto& z : h->Z) CHECK(dalloc(h, &z, (size_t)B * H));
   h->Hb.assign(h->L + 1, nullptr);
@@ -376,17 +403,17 @@ int build(Handle* h, const lcn_config* c) {
     }
   }
   CHECK(dalloc(h, &h->c123, 3 * F));
-  CHECK(dalloc(h, &h->stat_part, (size_t)cdiv(B, kLiftRows) * H));
+  CHECK(dalloc(h, &h->stat_part, (size_t)cdiv(B, kMinTileRows) * H));
   CHECK(dalloc(h, &h->bpart, (size_t)cdiv(B, kEwRows) * H));
   CHECK(dalloc(h, &h->col_part, (size_t)cdiv(B, kEwRows) * 64));
-  CHECK(dalloc(h, &h->loss_part, (size_t)cdiv(B, 64)));
+  h->loss_grid = (int)std::min<int64_t>(2048, cdiv(B, 4));
+  CHECK(dalloc(h, &h->loss_part, (size_t)h->loss_grid));
   CHECK(dalloc(h, &h->loss_sum, 4));
   CHECK(dalloc(h, &h->acc1, 2 * F));
   CHECK(dalloc(h, &h->acc2, 2 * F));
-  h->dw_nch_max = std::max(1, std::min(64, 8192 / std::max(1, h->nblk)));
-  CHECK(dalloc(h, &h->dw_part, (size_t)h->dw_nch_max * h->nblk * 4096));
-  h->outer_nch_max = 128;
-  CHECK(dalloc(h, &h->outer_part, (size_t)h->outer_nch_max * h->nslab * kJ * 3 * 64));
+  const size_t dw_elems = std::max((size_t)dw_chunks(h->nblk) * h->nblk,
+                                   (size_t)dw_chunks(h->nslab) * h->nslab) * 4096;
+  CHECK(dalloc(h, &h->dw_part, dw_elems));
   return LCN_OK;
 }
 
@@ -448,57 +475,82 @@ int bn_stats(Handle* h, int k, int B, int tile) {
   return LCN_OK;
 }
 
-int gemm(Handle* h, int k, int kindt, const float* X, bool pro, const BnStats* pst, float* Y,
-         const float* addsrc, bool stats, int B) {
-  const WLayer& Lr = h->wl[k];
+// One launch of the block-sparse MFMA GEMM: Y[:, so-slab] = sum over the CSR
+// list of X[:, si-slab] . block (+ bias / + addsrc), optional BN prologue on X
+// and BN partials in the epilogue.  `timer` < 0: not timed.
+struct GemmCall {
+  const float* X; int ldx;
+  const float* blocks; const int* ptr; const int2* idx; int n_out_slabs;
+  const float* bias; const BnStats* pro;
+  float* Y; int ldy; const float* addsrc; bool stats;
+  int timer; double flops_per_row;
+};
+
+int gemm(Handle* h, const GemmCall& c, int B) {
   GemmArgs a{};
-  a.X = X;
-  a.ldx = h->H;
-  const bool fwd = kindt == LCN_K_GEMM_FWD;
-  a.blocks = fwd ? Lr.blk_fwd : Lr.blk_bwd;
-  a.ptr = fwd ? h->fwd_ptr : h->bwd_ptr;
-  a.idx = fwd ? h->fwd_idx : h->bwd_idx;
-  a.bias = fwd ? h->theta + h->b_off[k] : nullptr;
-  a.pro_scale = pro ? pst->scale : nullptr;
-  a.pro_shift = pro ? pst->shift : nullptr;
+  a.X = c.X;
+  a.ldx = c.ldx;
+  a.blocks = c.blocks;
+  a.ptr = c.ptr;
+  a.idx = c.idx;
+  a.bias = c.bias;
+  a.pro_scale = c.pro ? c.pro->scale : nullptr;
+  a.pro_shift = c.pro ? c.pro->shift : nullptr;
   a.spj_in = h->spj;
   a.alpha = h->alpha;
-  a.Y = Y;
-  a.ldy = h->H;
-  a.addsrc = addsrc;
-  a.stat = stats ? h->stat_part : nullptr;
+  a.Y = c.Y;
+  a.ldy = c.ldy;
+  a.addsrc = c.addsrc;
+  a.stat = c.stats ? h->stat_part : nullptr;
   a.B = B;
-  a.n_out_slabs = h->nslab;
-  a.n_row_tiles = (int)cdiv(B, kGemmBM);
+  a.n_out_slabs = c.n_out_slabs;
+  a.variant = h->gemm_variant;
+  a.n_row_tiles = (int)cdiv(B, gemm_bs_rows(a.variant));
   hipEvent_t ev[2];
-  tstart(h, kindt, ev);
+  if (c.timer >= 0) tstart(h, c.timer, ev);
   launch_gemm_bs(a, h->stream);
-  tstop(h, kindt, ev, 2.0 * 4096.0 * h->nblk * B);  // 2*64*64 FLOP per block per row
+  if (c.timer >= 0) tstop(h, c.timer, ev, c.flops_per_row * B);
   return LCN_OK;
 }
 
-int gemm_dw(Handle* h, int k, const float* A, bool pro, const BnStats* pst, const float* D, int B) {
+// hidden layer k: forward (kindt = LCN_K_GEMM_FWD) or backward-data (LCN_K_GEMM_DX)
+int gemm_hidden(Handle* h, int k, int kindt, const float* X, const BnStats* pro, float* Y,
+                const float* addsrc, bool stats, int B) {
+  const WLayer& Lr = h->wl[k];
+  const bool fwd = kindt == LCN_K_GEMM_FWD;
+  GemmCall c{X, h->H, fwd ? Lr.blk_fwd : Lr.blk_bwd, fwd ? h->fwd_ptr : h->bwd_ptr,
+             fwd ? h->fwd_idx : h->bwd_idx, h->nslab, fwd ? h->theta + h->b_off[k] : nullptr,
+             pro, Y, h->H, addsrc, stats, kindt, 2.0 * 4096.0 * h->nblk};  // 2*64*64 per block
+  return gemm(h, c, B);
+}
+
+// dW_e of a layer from A (input activations, optional BN prologue) and D (dZ):
+// partial slabs per batch chunk, then a fixed-order reduce into the raw-gradient
+// vector (rows / columns past the valid range are padding and are dropped)
+int gemm_dw(Handle* h, const float* A, int lda, const BnStats* pro, const float* D, int ldd,
+            const int2* blk, int nblk, float* dW, int ld, int rows_valid, int cols_valid,
+            int B, bool timed) {
   GemmDwArgs a{};
   a.A = A;
-  a.lda = h->H;
+  a.lda = lda;
   a.D = D;
-  a.ldd = h->H;
-  a.pro_scale = pro ? pst->scale : nullptr;
-  a.pro_shift = pro ? pst->shift : nullptr;
+  a.ldd = ldd;
+  a.pro_scale = pro ? pro->scale : nullptr;
+  a.pro_shift = pro ? pro->shift : nullptr;
   a.spj_in = h->spj;
   a.alpha = h->alpha;
-  a.blk = h->blk;
-  a.nblk = h->nblk;
+  a.blk = blk;
+  a.nblk = nblk;
   a.B = B;
-  const int nch = std::max(1, std::min<int>(h->dw_nch_max, (int)cdiv(B, 64)));
+  const int nch = std::max(1, std::min<int>(dw_chunks(nblk), (int)cdiv(B, 64)));
   a.chunk_rows = (int)(cdiv(cdiv(B, nch), 64) * 64);
   a.nchunks = (int)cdiv(B, a.chunk_rows);
   a.part = h->dw_part;
   hipEvent_t ev[2];
-  tstart(h, LCN_K_GEMM_DW, ev);
+  if (timed) tstart(h, LCN_K_GEMM_DW, ev);
   launch_gemm_dw(a, h->stream);
-  tstop(h, LCN_K_GEMM_DW, ev, 2.0 * 4096.0 * h->nblk * B);  // 2*64*64 FLOP per block per row
-  launch_dw_reduce(h->dw_part, a.nchunks, h->nblk, h->blk, h->rg + h->wl[k].w_off, h->H, h->stream);
+  if (timed) tstop(h, LCN_K_GEMM_DW, ev, 2.0 * 4096.0 * nblk * B);
+  launch_dw_reduce(h->dw_part, a.nchunks, nblk, blk, dW, ld, rows_valid, cols_valid, h->stream);
   return LCN_OK;
 }
 
@@ -538,38 +590,31 @@ int forward(Handle* h, int B, bool with_labels, bool train) {
   hipStream_t s = h->stream;
   const int H = h->H, nl = h->nl;
   CHECK(prep_weights(h));
-  // lift (models_att.py:714-742)
-  ExpandArgs ea{};
-  ea.small = h->x;
-  ea.lds_small = kJ * h->inF;
-  ea.C = h->inF;
-  ea.coef = h->wl[0].coef;
-  ea.umask = h->umask_lift;
-  ea.bias = h->theta + h->b_off[0];
-  ea.out = h->Z[0];
-  ea.ldo = H;
-  ea.stat = h->batch_norm ? h->stat_part : nullptr;
-  ea.B = B;
-  ea.n_slabs = h->nslab;
-  launch_expand(ea, s);
-  CHECK(bn_stats(h, 0, B, kLiftRows));
+  const int tile = gemm_bs_rows(h->gemm_variant);
+  // lift z0 = x . W1e + b1 (models_att.py:714-729): x padded to one 64-wide slab
+  const double thin_flops = 2.0 * 4096.0 * h->nslab;
+  CHECK(gemm(h, GemmCall{h->x, 64, h->wl[0].blk_fwd, h->thin_ptr, h->thin_idx, h->nslab,
+                         h->theta + h->b_off[0], nullptr, h->Z[0], H, nullptr,
+                         (bool)h->batch_norm, -1, thin_flops}, B));
+  CHECK(bn_stats(h, 0, B, tile));
   launch_bn_act(h->Z[0], nullptr, h->Hb[0], h->bn[0].scale, h->bn[0].shift, h->F, h->alpha, B, H, s);
   // two_linear blocks (models_att.py:630-705)
   for (int l = 0; l < h->L; ++l) {
     const int k1 = 2 * l + 1, k2 = 2 * l + 2;
-    CHECK(gemm(h, k1, LCN_K_GEMM_FWD, h->Hb[l], false, nullptr, h->Z[k1], nullptr, h->batch_norm, B));
-    CHECK(bn_stats(h, k1, B, kGemmBM));
-    CHECK(gemm(h, k2, LCN_K_GEMM_FWD, h->Z[k1], true, &h->bn[k1], h->Z[k2], nullptr, h->batch_norm,
-               B));
-    CHECK(bn_stats(h, k2, B, kGemmBM));
+    CHECK(gemm_hidden(h, k1, LCN_K_GEMM_FWD, h->Hb[l], nullptr, h->Z[k1], nullptr, h->batch_norm, B));
+    CHECK(bn_stats(h, k1, B, tile));
+    CHECK(gemm_hidden(h, k2, LCN_K_GEMM_FWD, h->Z[k1], &h->bn[k1], h->Z[k2], nullptr,
+                      h->batch_norm, B));
+    CHECK(bn_stats(h, k2, B, tile));
     launch_bn_act(h->Z[k2], h->residual ? h->Hb[l] : nullptr, h->Hb[l + 1], h->bn[k2].scale,
                   h->bn[k2].shift, h->F, h->alpha, B, H, s);
   }
-  // output layer + loss (models_att.py:749-773, :356)
-  OutFwdArgs oa{};
-  oa.h = h->Hb[h->L];
-  oa.ldh = H;
-  oa.w4 = h->wl[nl - 1].dense_e;
+  // output layer y = h_L . W4e + b4 into a [B][64] buffer (51 used), then the
+  // output assembly, loss and d out (models_att.py:749-773, :356)
+  CHECK(gemm(h, GemmCall{h->Hb[h->L], H, h->wl[nl - 1].blk_fwd, h->out_ptr, h->out_idx, 1,
+                         nullptr, nullptr, h->yout, 64, nullptr, false, -1, thin_flops}, B));
+  OutAsmArgs oa{};
+  oa.y = h->yout;
   oa.b4 = h->theta + h->b_off[nl - 1];
   oa.x = h->x;
   oa.in_f = h->inF;
@@ -579,72 +624,42 @@ int forward(Handle* h, int B, bool with_labels, bool train) {
   oa.loss_part = with_labels ? h->loss_part : nullptr;
   oa.dscale = (float)(2.0 / ((double)B * h->world * 51.0));
   oa.B = B;
-  oa.n_in_slabs = h->nslab;
-  launch_out_fwd(oa, s);
-  if (with_labels) launch_loss_finalize(h->loss_part, (int)cdiv(B, 64), h->loss_sum, s);
+  const int ogrid = (int)std::min<int64_t>(h->loss_grid, cdiv(B, 4));
+  launch_out_assemble(oa, ogrid, s);
+  if (with_labels) launch_loss_finalize(h->loss_part, ogrid, h->loss_sum, s);
   return LCN_OK;
 }
 
 int backward(Handle* h, int B) {
   hipStream_t s = h->stream;
   const int nl = h->nl, L = h->L;
-  // output layer: dh_L = dy . W4e^T, dW4e = h_L^T dy, db4 = sum dy
-  ExpandArgs ea{};
-  ea.small = h->dy;
-  ea.lds_small = 51;
-  ea.C = 3;
-  ea.coef = h->wl[nl - 1].coef;
-  ea.umask = h->umask_out;
-  ea.out = h->DH;
-  ea.ldo = h->H;
-  ea.B = B;
-  ea.n_slabs = h->nslab;
-  launch_expand(ea, s);
-  OuterArgs oa{};
-  oa.big = h->Hb[L];
-  oa.ldb = h->H;
-  oa.small = h->dy;
-  oa.lds_small = 51;
-  oa.C = 3;
-  oa.umask = h->umask_out;
-  oa.B = B;
-  oa.nchunks = std::max(1, std::min<int>(h->outer_nch_max, (int)cdiv(B, 64)));
-  oa.chunk_rows = (int)(cdiv(cdiv(B, oa.nchunks), 64) * 64);
-  oa.nchunks = (int)cdiv(B, oa.chunk_rows);
-  oa.n_slabs = h->nslab;
-  oa.part = h->outer_part;
-  launch_outer(oa, s);
-  launch_outer_reduce(h->outer_part, oa.nchunks, h->nslab, 3, 1, h->rg + h->wl[nl - 1].w_off, s);
-  launch_colpart(h->dy, B, 51, 51, h->col_part, s);
+  const int H = h->H;
+  const WLayer& Lo = h->wl[nl - 1];
+  // output layer: dh_L = dy . W4e^T (dy padded to 64 columns), dW4e = h_L^T dy, db4 = sum dy
+  CHECK(gemm(h, GemmCall{h->dy, 64, Lo.blk_bwd, h->thin_ptr, h->thin_idx, h->nslab, nullptr,
+                         nullptr, h->DH, H, nullptr, false, -1, 0.0}, B));
+  CHECK(gemm_dw(h, h->Hb[L], H, nullptr, h->dy, 64, h->out_blk, h->nslab, h->rg + Lo.w_off, 51,
+                H, 51, B, false));
+  launch_colpart(h->dy, B, 51, 64, h->col_part, s);
   launch_colsum(h->col_part, (int)cdiv(B, kEwRows), 51, h->rg + h->b_off[nl - 1], s);
 
   for (int l = L - 1; l >= 0; --l) {
     const int k1 = 2 * l + 1, k2 = 2 * l + 2;
     // DH = dh_{l+1}: gradient of the block output
     CHECK(bn_back(h, k2, h->DH, B));                                   // DZ = dz_k2
-    CHECK(gemm_dw(h, k2, h->Z[k1], true, &h->bn[k1], h->DZ, B));       // dW_k2 = g^T dz
-    CHECK(gemm(h, k2, LCN_K_GEMM_DX, h->DZ, false, nullptr, h->DG, nullptr, false, B));  // dg
+    CHECK(gemm_dw(h, h->Z[k1], H, &h->bn[k1], h->DZ, H, h->blk, h->nblk,
+                  h->rg + h->wl[k2].w_off, H, H, H, B, true));         // dW_k2 = g^T dz
+    CHECK(gemm_hidden(h, k2, LCN_K_GEMM_DX, h->DZ, nullptr, h->DG, nullptr, false, B));  // dg
     CHECK(bn_back(h, k1, h->DG, B));                                   // DZ = dz_k1
-    CHECK(gemm_dw(h, k1, h->Hb[l], false, nullptr, h->DZ, B));         // dW_k1 = h_l^T dz
-    CHECK(gemm(h, k1, LCN_K_GEMM_DX, h->DZ, false, nullptr, h->DH, h->residual ? h->DH : nullptr,
-               false, B));                                             // dh_l (+ residual)
+    CHECK(gemm_dw(h, h->Hb[l], H, nullptr, h->DZ, H, h->blk, h->nblk,
+                  h->rg + h->wl[k1].w_off, H, H, H, B, true));         // dW_k1 = h_l^T dz
+    CHECK(gemm_hidden(h, k1, LCN_K_GEMM_DX, h->DZ, nullptr, h->DH,
+                      h->residual ? h->DH : nullptr, false, B));       // dh_l (+ residual)
   }
-  // lift: dz0, dW1e = x^T dz0, db1
+  // lift: dz0, dW1e = x^T dz0 (x padded: rows >= 17*in_F dropped), db1
   CHECK(bn_back(h, 0, h->DH, B));
-  OuterArgs la{};
-  la.big = h->DZ;
-  la.ldb = h->H;
-  la.small = h->x;
-  la.lds_small = kJ * h->inF;
-  la.C = h->inF;
-  la.umask = h->umask_lift;
-  la.B = B;
-  la.nchunks = oa.nchunks;
-  la.chunk_rows = oa.chunk_rows;
-  la.n_slabs = h->nslab;
-  la.part = h->outer_part;
-  launch_outer(la, s);
-  launch_outer_reduce(h->outer_part, la.nchunks, h->nslab, h->inF, 0, h->rg + h->wl[0].w_off, s);
+  CHECK(gemm_dw(h, h->x, 64, nullptr, h->DZ, H, h->lift_blk, h->nslab, h->rg + h->wl[0].w_off, H,
+                kJ * h->inF, H, B, false));
   return LCN_OK;
 }
 
@@ -676,7 +691,10 @@ int stage_inputs(Handle* h, const float* x, const float* lab, int64_t B, int fla
     return LCN_E_ARG;
   }
   const hipMemcpyKind kind = (flags & LCN_IN_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-  if (x) HIPC(hipMemcpyAsync(h->x, x, (size_t)B * kJ * h->inF * 4, kind, h->stream));
+  // x lands in the 64-column padded buffer of the lift GEMM (pads stay zero)
+  if (x)
+    HIPC(hipMemcpy2DAsync(h->x, 64 * sizeof(float), x, (size_t)kJ * h->inF * sizeof(float),
+                          (size_t)kJ * h->inF * sizeof(float), (size_t)B, kind, h->stream));
   if (lab) HIPC(hipMemcpyAsync(h->lab, lab, (size_t)B * 51 * 4, kind, h->stream));
   h->lastB = B;
   return LCN_OK;

@@ -9,7 +9,7 @@ namespace lcn {
 constexpr int kJ = 17;          // joints (models_att.py:512-513)
 constexpr int kSlab = 64;       // feature slab = MFMA tile edge; F is a multiple of it
 constexpr int kGemmBM = 128;    // batch rows per block-sparse GEMM tile
-constexpr int kLiftRows = 64;   // rows per lift-layer tile (BN partial granularity)
+constexpr int kMinTileRows = 64;  // smallest GEMM row tile (sizes the BN partial buffers)
 constexpr int kEwRows = 256;    // rows per tile of the BN-backward elementwise kernels
 
 // ----------------------------------------------------------------------------
@@ -31,8 +31,10 @@ struct GemmArgs {
   const float* addsrc;               // Y = acc (+ addsrc) ; may alias Y
   float2* stat;                      // BN partials [row_tiles][ldy] (sum, m2) or null
   int B; int n_out_slabs; int n_row_tiles;
+  int variant;                       // tile / pipeline variant (kernels_gemm.hip)
 };
 void launch_gemm_bs(const GemmArgs& a, hipStream_t s);
+int gemm_bs_rows(int variant);       // batch rows per workgroup tile of a variant
 
 // dWe blocks: part[chunk][blk][p][q] = sum_{b in chunk} A[b, si*64+p] * D[b, so*64+q]
 struct GemmDwArgs {
@@ -45,53 +47,30 @@ struct GemmDwArgs {
   float* part;                       // [nchunks][nblk][4096]
 };
 void launch_gemm_dw(const GemmDwArgs& a, hipStream_t s);
-// sum partials over chunks; write into dense dW [kin][ld] at (si*64+p, so*64+q)
+// sum partials over chunks; write into dense dW [rows][ld] at (si*64+p, so*64+q),
+// dropping rows >= rows_valid / columns >= cols_valid (padding of thin layers)
 void launch_dw_reduce(const float* part, int nchunks, int nblk, const int2* blk,
-                      float* dW, int ld, hipStream_t s);
+                      float* dW, int ld, int rows_valid, int cols_valid, hipStream_t s);
 
 // ----------------------------------------------------------------------------
-// Small-K layers (lift 34->H and the output layer's dX), VALU.
-// out[b, s*64+f] = sum_{u,c} small[b, u*C+c] * coef[s][u][c][f] (+ bias)
+// The thin layers run on the same MFMA kernels with the narrow side padded to
+// one 64-wide slab: the lift's input x [B][17*in_F] lives in a [B][64] buffer
+// (K = 34 -> 64) and the output layer's 51 columns in [B][64] buffers.
 // ----------------------------------------------------------------------------
-struct ExpandArgs {
-  const float* small; int lds_small; int C;
-  const float* coef;                 // [n_slabs][J][C][64]
-  const unsigned* umask;             // [n_slabs] bit u = joint u contributes
-  const float* bias;                 // or null
-  float* out; int ldo;
-  float2* stat;                      // [B/64 tiles][ldo] or null
-  int B; int n_slabs;
-};
-void launch_expand(const ExpandArgs& a, hipStream_t s);
-
-// part[chunk][s][u][c][f] = sum_b big[b, s*64+f] * small[b, u*C+c] for u in umask[s]
-struct OuterArgs {
-  const float* big; int ldb;
-  const float* small; int lds_small; int C;
-  const unsigned* umask;
-  int B; int chunk_rows; int nchunks; int n_slabs;
-  float* part;                       // [nchunks][n_slabs][J*C][64]
-};
-void launch_outer(const OuterArgs& a, hipStream_t s);
-// reduce over chunks and scatter: mode 0 (lift): dW[(u*C+c)][s*64+f], ld = n_slabs*64
-//                                 mode 1 (out):  dW[s*64+f][u*C+c],   ld = J*C
-void launch_outer_reduce(const float* part, int nchunks, int n_slabs, int C, int mode,
-                         float* dW, hipStream_t s);
-
-// Output layer forward + loss + dy (models_att.py:749-773, :356)
-struct OutFwdArgs {
-  const float* h; int ldh;           // [B][H]
-  const float* w4;                   // dense masked W4e [H][51]
-  const float* b4;
-  const float* x; int in_f;          // [B][J*in_f]
+// y = h . W4e from the GEMM; out[b, 3j+c] = (c < 2 ? x[b, in_f*j+c] : 0) + (y + b4);
+// loss partials and dy = dscale * (out - lab) (padded [B][64]) (models_att.py:765-773, :356)
+struct OutAsmArgs {
+  const float* y;                    // [B][64] (51 used)
+  const float* b4;                   // [51]
+  const float* x; int in_f;          // x padded [B][64]
   const float* lab;                  // [B][51] or null
   float* out;                        // [B][51]
-  float* dy;                         // [B][51] or null
+  float* dy;                         // [B][64] or null
   double* loss_part;                 // [gridDim] or null
   float dscale;                      // 2 / (B_global * 51)
-  int B; int n_in_slabs;
+  int B;
 };
-void launch_out_fwd(const OutFwdArgs& a, hipStream_t s);
+void launch_out_assemble(const OutAsmArgs& a, int grid, hipStream_t s);
 
 // ----------------------------------------------------------------------------
 // BatchNorm (batch statistics), activation, BN backward
@@ -133,10 +112,12 @@ struct WLayer {            // one linear layer's weight
   int64_t w_off;           // offset in the flat parameter vector
   int kin, nout, fin, fout;
   int kind;                // 0 lift, 1 hidden, 2 output
-  float* dense_e;          // dense masked effective weight (lift/out) or null
-  float* coef;             // expand coefficients (lift: fwd; out: bwd-dx) or null
-  float* blk_fwd;          // hidden: packed [nblk][q][p]
-  float* blk_bwd;          // hidden: packed [nblk][p][q]
+  // packed 64x64 blocks of W_e, K-contiguous ([n][k]) for the MFMA kernels:
+  //   hidden: blk_fwd [nblk][q][p], blk_bwd [nblk][p][q]
+  //   lift:   blk_fwd [nslab][f][k = u*in_F + c] (k >= 17*in_F zero)
+  //   output: blk_fwd [nslab][c'][p], blk_bwd [nslab][p][c'] (c' >= 51 zero)
+  float* blk_fwd;
+  float* blk_bwd;
   const int2* blk;         // hidden: (si, so) per block (device)
   int nblk;
 };

@@ -3,7 +3,7 @@ python resources.py [files...]"""
 import os, re, subprocess, sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-files = sys.argv[1:] or ["kernels_gemm.hip", "kernels_io.hip", "kernels_elem.hip", "kernels_param.hip"]
+files = sys.argv[1:] or ["gemm_bs.hip", "kernels_gemm.hip", "kernels_io.hip", "kernels_elem.hip", "kernels_param.hip"]
 for f in files:
     r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950",
                         "-I../../include", "-c", f, "-o", "/dev/null",
