@@ -87,6 +87,11 @@ int main(int argc, char** argv) {
   float* bias = dev(hb);
   float* sc = dev(hs);
   float* sh = dev(hh);
+  std::vector<float> hc(3 * F), hm(F, 0.f), hr(F, 1.f);
+  for (int f = 0; f < F; ++f) { hc[f] = 1.f; hc[F + f] = 0.01f * U(rng); hc[2 * F + f] = 0.01f * U(rng); }
+  float* c123 = dev(hc);
+  float* mean = dev(hm);
+  float* rstd = dev(hr);
   int2* dblk = dev(blk);
   int* dfp = dev(fptr);
   int* dbp = dev(bptr);
@@ -95,7 +100,7 @@ int main(int argc, char** argv) {
   float* Y;
   CK(hipMalloc(&Y, (size_t)B * H * 4));
   float2* stat;
-  CK(hipMalloc(&stat, (size_t)(B / 64 + 1) * H * 8));
+  CK(hipMalloc(&stat, (size_t)(B / 128 + 1) * H * 8));
   const int nch = std::max(1, std::min(64, 8192 / nblk));
   float* part;
   CK(hipMalloc(&part, (size_t)nch * nblk * 4096 * 4));
@@ -108,7 +113,9 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   const double flop = 2.0 * 4096.0 * nblk * B;
 
-  auto mk = [&](bool fwd, bool pro, bool stats, int variant) {
+  // kind 0: forward (bias, EPI_BNFWD); 1: backward-data (+residual, EPI_BNBACK)
+  auto mk = [&](int kind, int pro, int variant) {
+    const bool fwd = kind == 0;
     GemmArgs a{};
     a.X = X;
     a.ldx = H;
@@ -116,6 +123,7 @@ int main(int argc, char** argv) {
     a.ptr = fwd ? dfp : dbp;
     a.idx = fwd ? dfi : dbi;
     a.bias = fwd ? bias : nullptr;
+    a.pro_mode = pro;
     a.pro_scale = pro ? sc : nullptr;
     a.pro_shift = pro ? sh : nullptr;
     a.spj_in = 1;
@@ -123,7 +131,14 @@ int main(int argc, char** argv) {
     a.Y = Y;
     a.ldy = H;
     a.addsrc = fwd ? nullptr : Y;
-    a.stat = stats ? stat : nullptr;
+    a.epi_mode = fwd ? EPI_BNFWD : EPI_BNBACK;
+    a.stat = stat;
+    a.epi_z = X2;
+    a.epi_scale = sc;
+    a.epi_shift = sh;
+    a.epi_mean = mean;
+    a.epi_rstd = rstd;
+    a.epi_F = F;
     a.B = B;
     a.n_out_slabs = J;
     a.variant = variant;
@@ -137,6 +152,18 @@ int main(int argc, char** argv) {
   d.ldd = H;
   d.spj_in = 1;
   d.alpha = 0.2f;
+  d.d_z = X;
+  d.d_scale = sc;
+  d.d_shift = sh;
+  d.d_c123 = c123;
+  d.d_F = F;
+  std::vector<int> hwr(nblk, 0), seen(J, 0);
+  for (int b = 0; b < nblk; ++b)
+    if (!seen[blk[b].y]) { seen[blk[b].y] = 1; hwr[b] = 1; }
+  d.dz_writer = dev(hwr);
+  float* dzo;
+  CK(hipMalloc(&dzo, (size_t)B * H * 4));
+  d.dz_out = dzo;
   d.blk = dblk;
   d.nblk = nblk;
   d.B = B;
@@ -144,27 +171,29 @@ int main(int argc, char** argv) {
   d.nchunks = (B + d.chunk_rows - 1) / d.chunk_rows;
   d.part = part;
 
-  struct Case { const char* name; int kind; bool pro; bool stats; int variant; };
+  struct Case { const char* name; int kind; int pro; int variant; };
   std::vector<Case> cases;
-  const int nvar = argc > 4 ? std::atoi(argv[4]) : 3;
+  const int nvar = argc > 4 ? std::atoi(argv[4]) : 1;
   for (int v = 0; v < nvar; ++v) {
-    cases.push_back({"fwd raw +stats", 0, false, true, v});
-    cases.push_back({"fwd bnact +stats", 0, true, true, v});
-    cases.push_back({"dx +residual", 1, false, false, v});
+    cases.push_back({"fwd raw +bnstat", 0, PRO_RAW, v});
+    cases.push_back({"fwd bnact +bnstat", 0, PRO_BNACT, v});
+    cases.push_back({"dx raw +bnback", 1, PRO_RAW, v});
   }
-  cases.push_back({"dw raw", 2, false, false, 0});
-  cases.push_back({"dw bnact", 2, true, false, 0});
+  cases.push_back({"dw raw", 2, PRO_RAW, 0});
+  cases.push_back({"dw bnact x bnback", 2, PRO_BNACT, 0});
+  cases.push_back({"dw raw x bnback", 2, PRO_BNBACK, 0});
   const int rounds = 3;
   for (int r = 0; r < rounds; ++r) {
     for (const Case& c : cases) {
       auto run = [&]() {
         if (c.kind == 2) {
-          d.pro_scale = c.pro ? sc : nullptr;
-          d.pro_shift = c.pro ? sh : nullptr;
+          d.pro_scale = c.pro == PRO_BNACT ? sc : nullptr;
+          d.pro_shift = c.pro == PRO_BNACT ? sh : nullptr;
+          d.d_bnback = c.pro != PRO_RAW;
           launch_gemm_dw(d, s);
-          launch_dw_reduce(part, d.nchunks, nblk, dblk, dW, H, s);
+          launch_dw_reduce(part, d.nchunks, nblk, dblk, dW, H, H, H, s);
         } else {
-          launch_gemm_bs(mk(c.kind == 0, c.pro, c.stats, c.variant), s);
+          launch_gemm_bs(mk(c.kind, c.pro, c.variant), s);
         }
       };
       run();
@@ -178,16 +207,6 @@ int main(int argc, char** argv) {
       ms /= iters;
       std::printf("round %d v%d %-18s %8.1f us  %6.1f TFLOP/s  (%.1f%% of 157.3)\n", r, c.variant, c.name,
                   ms * 1e3, flop / (ms * 1e-3) / 1e12, 100.0 * flop / (ms * 1e-3) / 1e12 / 157.3);
-      if (r == 0 && c.kind == 0) {  // cross-check every variant's forward output against v0
-        static std::vector<float> ref[2];
-        std::vector<float> got((size_t)B * H);
-        CK(hipMemcpy(got.data(), Y, got.size() * 4, hipMemcpyDeviceToHost));
-        std::vector<float>& rf = ref[c.pro ? 1 : 0];
-        if (rf.empty()) rf = got;
-        double md = 0;
-        for (size_t i = 0; i < got.size(); ++i) md = std::max(md, (double)std::fabs(got[i] - rf[i]));
-        std::printf("   max |Y - Y_v0| = %.3e\n", md);
-      }
     }
   }
   CK(hipGetLastError());

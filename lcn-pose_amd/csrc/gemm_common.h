@@ -24,6 +24,37 @@ __device__ __forceinline__ float4 bnact4(float4 v, float4 sc, float4 sh, float a
   return v;
 }
 
+// BN + LeakyReLU backward:
+//   u = scale*z + shift,  du = u > 0 ? dh : alpha*dh,  dz = c1*du + c2 + c3*z
+struct BnBackCoef { float4 sc, sh, c1, c2, c3; };
+
+__device__ __forceinline__ BnBackCoef load_bnback_coef(const float* scale, const float* shift,
+                                                       const float* c123, int F, int ch) {
+  BnBackCoef c;
+  c.sc = *(const float4*)(scale + ch);
+  c.sh = *(const float4*)(shift + ch);
+  c.c1 = *(const float4*)(c123 + ch);
+  c.c2 = *(const float4*)(c123 + F + ch);
+  c.c3 = *(const float4*)(c123 + 2 * F + ch);
+  return c;
+}
+
+__device__ __forceinline__ float bnback1(float dh, float z, float sc, float sh, float c1, float c2,
+                                         float c3, float alpha) {
+  const float u = fmaf(z, sc, sh);
+  const float du = u > 0.f ? dh : dh * alpha;
+  return fmaf(c1, du, fmaf(c3, z, c2));
+}
+
+__device__ __forceinline__ float4 bnback4(float4 dh, float4 z, const BnBackCoef& c, float alpha) {
+  float4 r;
+  r.x = bnback1(dh.x, z.x, c.sc.x, c.sh.x, c.c1.x, c.c2.x, c.c3.x, alpha);
+  r.y = bnback1(dh.y, z.y, c.sc.y, c.sh.y, c.c1.y, c.c2.y, c.c3.y, alpha);
+  r.z = bnback1(dh.z, z.z, c.sc.z, c.sh.z, c.c1.z, c.c2.z, c.c3.z, alpha);
+  r.w = bnback1(dh.w, z.w, c.sc.w, c.sh.w, c.c1.w, c.c2.w, c.c3.w, alpha);
+  return r;
+}
+
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), 0, 0, 0)
 
 // 4 k-steps (one float4 of A and of two B columns) into two 32x32 accumulators
@@ -37,18 +68,29 @@ __device__ __forceinline__ float4 bnact4(float4 v, float4 sc, float4 sh, float a
   ACC0 = MFMA32((AV).w, (B0).w, ACC0);       \
   ACC1 = MFMA32((AV).w, (B1).w, ACC1);
 
+// Sum a per-lane value over the 128 rows of the tile for the lane's column:
+// the two half-waves, then the 4 waves through LDS (fixed order).
+__device__ __forceinline__ float tile_colsum(float v, float* red, int w, int lr, int h, int half) {
+  v += __shfl_xor(v, 32);
+  if (h == 0) red[w * 64 + half * 32 + lr] = v;
+  __syncthreads();
+  const int c = half * 32 + lr;
+  return (red[c] + red[64 + c]) + (red[128 + c] + red[192 + c]);
+}
+
 // Epilogue of a 128-row x 64-column tile computed by 4 waves of 32 x 64
 // (acc0: columns 0-31, acc1: 32-63).  C/D map of the 32x32 MFMA: column =
 // lane&31, row = (k&3) + 8(k>>2) + 4(lane>>5).  Adds bias (forward) or the
-// residual gradient (backward), stores, and writes the BN partials of the
-// tile: (sum, sum of squared deviations about the tile mean) per column.
+// residual gradient (backward), stores, then writes the tile partials:
+//   EPI_BNFWD:  (sum, sum of squared deviations about the tile mean) of Y
+//   EPI_BNBACK: (sum du, sum du*zhat) for the BN layer below, with the stored
+//               value as its incoming gradient dh
 __device__ __forceinline__ void gemm_epilogue_32x64(const GemmArgs& a, f32x16& acc0, f32x16& acc1,
                                                     int rt, int so, int row0, int w, int lr, int h,
                                                     float* smem) {
   const int B = a.B, ldy = a.ldy;
   float* __restrict__ Y = a.Y;
   const float* __restrict__ addsrc = a.addsrc;
-  float2* __restrict__ stat = a.stat;
   const int ncol0 = so * kSlab + lr, ncol1 = ncol0 + 32;
   const float bias0 = a.bias ? a.bias[ncol0] : 0.f;
   const float bias1 = a.bias ? a.bias[ncol1] : 0.f;
@@ -68,106 +110,63 @@ __device__ __forceinline__ void gemm_epilogue_32x64(const GemmArgs& a, f32x16& a
     acc0[k] = v0;
     acc1[k] = v1;
   }
-  if (stat == nullptr) return;
-  const int nval = min(128, B - row0);
-  s0 += __shfl_xor(s0, 32);
-  s1 += __shfl_xor(s1, 32);
-  __syncthreads();
-  float* red = smem;  // [4][64] sums, then [4][64] m2
-  if (h == 0) { red[w * 64 + lr] = s0; red[w * 64 + 32 + lr] = s1; }
-  __syncthreads();
-  const float tot0 = (red[lr] + red[64 + lr]) + (red[128 + lr] + red[192 + lr]);
-  const float tot1 = (red[32 + lr] + red[96 + lr]) + (red[160 + lr] + red[224 + lr]);
-  const float mean0 = tot0 / (float)nval, mean1 = tot1 / (float)nval;
-  float m0 = 0.f, m1 = 0.f;
+  if (a.epi_mode == EPI_NONE) return;
+  float2* __restrict__ stat = a.stat;
+  float* red = smem;  // [4][64]
+  __syncthreads();    // all waves are done with the staging LDS
+  if (a.epi_mode == EPI_BNFWD) {
+    const int nval = min(128, B - row0);
+    const float tot0 = tile_colsum(s0, red, w, lr, h, 0);
+    const float tot1 = tile_colsum(s1, red, w, lr, h, 1);
+    const float mean0 = tot0 / (float)nval, mean1 = tot1 / (float)nval;
+    float m0 = 0.f, m1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int row = row0 + 32 * w + (k & 3) + 8 * (k >> 2) + 4 * h;
+      if (row < B) {
+        const float d0 = acc0[k] - mean0, d1 = acc1[k] - mean1;
+        m0 = fmaf(d0, d0, m0);
+        m1 = fmaf(d1, d1, m1);
+      }
+    }
+    __syncthreads();
+    const float q0 = tile_colsum(m0, red + 256, w, lr, h, 0);
+    const float q1 = tile_colsum(m1, red + 256, w, lr, h, 1);
+    if (w == 0 && h == 0) {
+      stat[(size_t)rt * ldy + ncol0] = make_float2(tot0, q0);
+      stat[(size_t)rt * ldy + ncol1] = make_float2(tot1, q1);
+    }
+    return;
+  }
+  // EPI_BNBACK: du = dh * leaky'(u(z)), zhat = (z - mean) * rstd of the layer below
+  const float* __restrict__ Z = a.epi_z;
+  const int ch0 = ncol0 % a.epi_F, ch1 = ncol1 % a.epi_F;
+  const float sc0 = a.epi_scale[ch0], sh0 = a.epi_shift[ch0], mu0 = a.epi_mean[ch0], rs0 = a.epi_rstd[ch0];
+  const float sc1 = a.epi_scale[ch1], sh1 = a.epi_shift[ch1], mu1 = a.epi_mean[ch1], rs1 = a.epi_rstd[ch1];
+  const float al = a.alpha;
+  float p0 = 0.f, p1 = 0.f, q0 = 0.f, q1 = 0.f;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int row = row0 + 32 * w + (k & 3) + 8 * (k >> 2) + 4 * h;
     if (row < B) {
-      const float d0 = acc0[k] - mean0, d1 = acc1[k] - mean1;
-      m0 = fmaf(d0, d0, m0);
-      m1 = fmaf(d1, d1, m1);
+      const size_t o = (size_t)row * ldy;
+      const float z0 = Z[o + ncol0], z1 = Z[o + ncol1];
+      const float du0 = fmaf(z0, sc0, sh0) > 0.f ? acc0[k] : acc0[k] * al;
+      const float du1 = fmaf(z1, sc1, sh1) > 0.f ? acc1[k] : acc1[k] * al;
+      p0 += du0;
+      p1 += du1;
+      q0 = fmaf(du0, (z0 - mu0) * rs0, q0);
+      q1 = fmaf(du1, (z1 - mu1) * rs1, q1);
     }
   }
-  m0 += __shfl_xor(m0, 32);
-  m1 += __shfl_xor(m1, 32);
-  float* red2 = smem + 256;
-  if (h == 0) { red2[w * 64 + lr] = m0; red2[w * 64 + 32 + lr] = m1; }
+  const float P0 = tile_colsum(p0, red, w, lr, h, 0);
+  const float P1 = tile_colsum(p1, red, w, lr, h, 1);
   __syncthreads();
+  const float Q0 = tile_colsum(q0, red + 256, w, lr, h, 0);
+  const float Q1 = tile_colsum(q1, red + 256, w, lr, h, 1);
   if (w == 0 && h == 0) {
-    const float q0 = (red2[lr] + red2[64 + lr]) + (red2[128 + lr] + red2[192 + lr]);
-    const float q1 = (red2[32 + lr] + red2[96 + lr]) + (red2[160 + lr] + red2[224 + lr]);
-    stat[(size_t)rt * ldy + ncol0] = make_float2(tot0, q0);
-    stat[(size_t)rt * ldy + ncol1] = make_float2(tot1, q1);
-  }
-}
-
-// Epilogue of a 256-row x 64-column tile: 4 waves x 64 rows; per wave acc0x
-// covers its rows 0-31 and acc1x rows 32-63 (x = column half).
-__device__ __forceinline__ void gemm_epilogue_64x64(const GemmArgs& a, f32x16& acc00, f32x16& acc01,
-                                                    f32x16& acc10, f32x16& acc11, int rt, int so,
-                                                    int row0, int w, int lr, int h, float* smem) {
-  const int B = a.B, ldy = a.ldy;
-  float* __restrict__ Y = a.Y;
-  const float* __restrict__ addsrc = a.addsrc;
-  float2* __restrict__ stat = a.stat;
-  const int ncol0 = so * kSlab + lr, ncol1 = ncol0 + 32;
-  const float bias0 = a.bias ? a.bias[ncol0] : 0.f;
-  const float bias1 = a.bias ? a.bias[ncol1] : 0.f;
-  const int rb = row0 + 64 * w + 4 * h;
-  float s0 = 0.f, s1 = 0.f;
-#define EPI_STORE(ACC0, ACC1, ROFF)                                         \
-  _Pragma("unroll") for (int k = 0; k < 16; ++k) {                         \
-    const int row = rb + (ROFF) + (k & 3) + 8 * (k >> 2);                  \
-    float v0 = ACC0[k] + bias0, v1 = ACC1[k] + bias1;                      \
-    if (row < B) {                                                         \
-      const size_t o = (size_t)row * ldy;                                  \
-      if (addsrc) { v0 += addsrc[o + ncol0]; v1 += addsrc[o + ncol1]; }    \
-      Y[o + ncol0] = v0;                                                   \
-      Y[o + ncol1] = v1;                                                   \
-      s0 += v0;                                                            \
-      s1 += v1;                                                            \
-    }                                                                      \
-    ACC0[k] = v0;                                                          \
-    ACC1[k] = v1;                                                          \
-  }
-  EPI_STORE(acc00, acc01, 0)
-  EPI_STORE(acc10, acc11, 32)
-#undef EPI_STORE
-  if (stat == nullptr) return;
-  const int nval = min(256, B - row0);
-  s0 += __shfl_xor(s0, 32);
-  s1 += __shfl_xor(s1, 32);
-  __syncthreads();
-  float* red = smem;  // [4][64] sums, then [4][64] m2
-  if (h == 0) { red[w * 64 + lr] = s0; red[w * 64 + 32 + lr] = s1; }
-  __syncthreads();
-  const float tot0 = (red[lr] + red[64 + lr]) + (red[128 + lr] + red[192 + lr]);
-  const float tot1 = (red[32 + lr] + red[96 + lr]) + (red[160 + lr] + red[224 + lr]);
-  const float mean0 = tot0 / (float)nval, mean1 = tot1 / (float)nval;
-  float m0 = 0.f, m1 = 0.f;
-#define EPI_M2(ACC0, ACC1, ROFF)                                            \
-  _Pragma("unroll") for (int k = 0; k < 16; ++k) {                         \
-    const int row = rb + (ROFF) + (k & 3) + 8 * (k >> 2);                  \
-    if (row < B) {                                                         \
-      const float d0 = ACC0[k] - mean0, d1 = ACC1[k] - mean1;              \
-      m0 = fmaf(d0, d0, m0);                                               \
-      m1 = fmaf(d1, d1, m1);                                               \
-    }                                                                      \
-  }
-  EPI_M2(acc00, acc01, 0)
-  EPI_M2(acc10, acc11, 32)
-#undef EPI_M2
-  m0 += __shfl_xor(m0, 32);
-  m1 += __shfl_xor(m1, 32);
-  float* red2 = smem + 256;
-  if (h == 0) { red2[w * 64 + lr] = m0; red2[w * 64 + 32 + lr] = m1; }
-  __syncthreads();
-  if (w == 0 && h == 0) {
-    const float q0 = (red2[lr] + red2[64 + lr]) + (red2[128 + lr] + red2[192 + lr]);
-    const float q1 = (red2[32 + lr] + red2[96 + lr]) + (red2[160 + lr] + red2[224 + lr]);
-    stat[(size_t)rt * ldy + ncol0] = make_float2(tot0, q0);
-    stat[(size_t)rt * ldy + ncol1] = make_float2(tot1, q1);
+    stat[(size_t)rt * ldy + ncol0] = make_float2(P0, Q0);
+    stat[(size_t)rt * ldy + ncol1] = make_float2(P1, Q1);
   }
 }
 

@@ -1,89 +1,165 @@
 // BatchNorm with batch statistics, LeakyReLU, residual and their backward
 // (gfx950).  Replaces Keras BatchNormalization(axis=-1) in training mode on
-// the [B, 17, F] view (models_att.py:588-612; tf.nn.moments two-pass mean /
-// biased variance, tf.nn.batch_normalization's x*inv + (beta - mean*inv)),
+// the [B, 17, F] view (models_att.py:588-612; tf.nn.moments mean / biased
+// variance, tf.nn.batch_normalization's x*inv + (beta - mean*inv)),
 // tf.nn.leaky_relu(alpha=0.2) and the residual add (models_att.py:704).
 //
-// Statistics are reduced in two levels: per-tile (sum, sum of squared
-// deviations about the tile mean) written by the producing kernel's
-// epilogue, then merged here in float64 (exact decomposition, no E[z^2]-mu^2
-// cancellation).  With several GPUs the merge is split into phases around an
-// RCCL all-reduce of the float64 partial sums (SyncBN).
+// Statistics are reduced in three levels: per 128-row tile the producing
+// GEMM's epilogue writes (sum, sum of squared deviations about the tile mean)
+// -- or, backward, (sum du, sum du*zhat) -- as float; colreduce merges the
+// tiles of every column in float64; the channel kernels merge the 17 joint
+// columns of a channel and finish.  The forward merge uses
+//   sum_b (z_b - mu)^2 = sum_t [M2_t + s_t^2 / n_t] - S^2 / N
+// in float64: each term is exact to ~1e-16 relative, so the cancellation of
+// the last difference costs nothing at float output precision.  With several
+// GPUs the channel sums are all-reduced (RCCL, float64) between the phases
+// (SyncBN): one all-reduce of 2F doubles per BN layer and direction.
 #include <algorithm>
 #include "lcn_internal.h"
 
 namespace lcn {
 
-__device__ __forceinline__ double block_sum_d(double v, double* red) {
-  // 256 threads
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  __syncthreads();
-  if (l == 0) red[w] = v;
-  __syncthreads();
-  return (red[0] + red[1]) + (red[2] + red[3]);
-}
-
-// One workgroup per channel ch; entries (tile t, joint-slab j) at column j*F + ch.
-__global__ __launch_bounds__(256) void bn_finalize_kernel(
-    const float2* __restrict__ part, int n_tiles, int tile_rows, int B, int H, int F,
-    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, double count,
-    double* acc1, double* acc2, int phase, BnStats st) {
-  __shared__ double red[4];
-  const int ch = blockIdx.x;
-  const int J = H / F;
-  const int n = n_tiles * J;
-  double mu = 0.0, s2 = 0.0;
-  if (phase == 0 || phase == 1) {
-    double s1 = 0.0;
-    for (int e = threadIdx.x; e < n; e += 256) {
-      const int t = e / J, j = e - t * J;
-      s1 += (double)part[(size_t)t * H + j * F + ch].x;
-    }
-    s1 = block_sum_d(s1, red);
-    if (phase == 1) {
-      if (threadIdx.x == 0) acc1[ch] = s1;
-      return;
-    }
-    mu = s1 / count;
-  }
-  if (phase == 2) mu = acc1[ch] / count;
-  if (phase == 0 || phase == 2) {
-    double q = 0.0;
-    for (int e = threadIdx.x; e < n; e += 256) {
-      const int t = e / J, j = e - t * J;
-      const float2 p = part[(size_t)t * H + j * F + ch];
-      const double nt = (double)min(tile_rows, B - t * tile_rows);
-      const double d = (double)p.x / nt - mu;
-      q += (double)p.y + nt * d * d;
-    }
-    s2 = block_sum_d(q, red);
-    if (phase == 2) {
-      if (threadIdx.x == 0) acc2[ch] = s2;
-      return;
-    }
-  }
-  if (phase == 3) { mu = acc1[ch] / count; s2 = acc2[ch]; }
-  if (threadIdx.x == 0) {
-    const float mean = (float)mu;
-    const float var = (float)(s2 / count);
-    const float rstd = 1.0f / sqrtf(var + eps);   // rsqrt(variance + epsilon)
-    const float inv = rstd * gamma[ch];           // inv *= scale
-    st.mean[ch] = mean;
-    st.rstd[ch] = rstd;
-    st.scale[ch] = inv;
-    st.shift[ch] = beta[ch] - mean * inv;         // offset - mean * inv
-  }
-}
-
-void launch_bn_finalize(const float2* part, int n_row_tiles, int tile_rows, int B, int H, int F,
-                        const float* gamma, const float* beta, float eps, double count,
-                        double* acc1, double* acc2, int phase, BnStats st, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(F), dim3(256), 0, s, part, n_row_tiles, tile_rows, B,
-                     H, F, gamma, beta, eps, count, acc1, acc2, phase, st);
-}
-
 __device__ __forceinline__ float leaky(float u, float alpha) { return u > 0.f ? u : u * alpha; }
+
+// out[col] = sum over tiles of part[t][col] in float64, 64 columns per
+// workgroup, 16 waves striding the tiles, fixed-order combine (deterministic).
+//   mode 0: (sum x, sum y)          mode 1: (sum x, sum (y + x^2 / n_t))
+__global__ __launch_bounds__(1024) void colreduce_kernel(const float2* __restrict__ part,
+                                                         int n_tiles, int tile_rows, int B, int H,
+                                                         int mode, double2* __restrict__ out) {
+  __shared__ double2 red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  double a = 0.0, b = 0.0;
+  if (col < H) {
+#pragma unroll 4
+    for (int t = w; t < n_tiles; t += 16) {
+      const float2 p = part[(size_t)t * H + col];
+      a += (double)p.x;
+      if (mode == 1) {
+        const double nt = (double)min(tile_rows, B - t * tile_rows);
+        b += (double)p.y + (double)p.x * (double)p.x / nt;
+      } else {
+        b += (double)p.y;
+      }
+    }
+  }
+  red[w][lane] = make_double2(a, b);
+  __syncthreads();
+  if (w == 0 && col < H) {
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { sa += red[i][lane].x; sb += red[i][lane].y; }
+    out[col] = make_double2(sa, sb);
+  }
+}
+
+void launch_colreduce(const float2* part, int n_tiles, int tile_rows, int B, int H, int mode,
+                      double2* out, hipStream_t s) {
+  hipLaunchKernelGGL(colreduce_kernel, dim3((H + 63) / 64), dim3(1024), 0, s, part, n_tiles,
+                     tile_rows, B, H, mode, out);
+}
+
+// Forward BN finish per channel ch (one thread each).  Phase 0: complete;
+// 1: local channel sums -> acc[2F] (and stop); 2: finish from the all-reduced acc.
+// zsum (when given) receives the per-column sums of z (bias-gradient term of
+// the backward).
+__global__ void bn_fwd_finalize_kernel(const double2* __restrict__ col, int H, int F, int phase,
+                                       double count, const float* __restrict__ gamma,
+                                       const float* __restrict__ beta, float eps, double* acc,
+                                       BnStats st, double* __restrict__ zsum) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= F) return;
+  const int J = H / F;
+  double S = 0.0, Q = 0.0;
+  if (phase <= 1) {
+    for (int j = 0; j < J; ++j) {
+      const double2 c = col[j * F + ch];
+      S += c.x;
+      Q += c.y;
+      if (zsum) zsum[j * F + ch] = c.x;
+    }
+    if (phase == 1) { acc[ch] = S; acc[F + ch] = Q; return; }
+  } else {
+    S = acc[ch];
+    Q = acc[F + ch];
+  }
+  const double mu = S / count;
+  const double var = fmax(0.0, Q / count - mu * mu);
+  const float mean = (float)mu;
+  const float rstd = 1.0f / sqrtf((float)var + eps);  // rsqrt(variance + epsilon)
+  const float inv = rstd * gamma[ch];                  // inv *= scale
+  st.mean[ch] = mean;
+  st.rstd[ch] = rstd;
+  st.scale[ch] = inv;
+  st.shift[ch] = beta[ch] - mean * inv;                // offset - mean * inv
+}
+
+void launch_bn_fwd_finalize(const double2* col, int H, int F, int phase, double count,
+                            const float* gamma, const float* beta, float eps, double* acc,
+                            BnStats st, double* zsum, hipStream_t s) {
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((F + 255) / 256), dim3(256), 0, s, col, H, F,
+                     phase, count, gamma, beta, eps, acc, st, zsum);
+}
+
+// Backward BN finish per channel:  dz = c1*du + c2 + c3*z,
+//   c1 = gamma*rstd, c3 = -c1*rstd*S2/N, c2 = -c1*S1/N - c3*mean,
+//   S1 = sum du = dbeta, S2 = sum du*zhat = dgamma.
+// The bias gradient of the layer is sum_b dz per column:
+//   db[col] = c1 * sum du[col] + B_local * c2 + c3 * sum z[col].
+// dgamma / dbeta / db are the LOCAL contributions (the raw-gradient vector is
+// all-reduced later); c123 uses the global sums.  bn = 0 (no BatchNorm):
+// dz = du and only db is written.  Phases as bn_fwd_finalize.
+__global__ void bn_bwd_finalize_kernel(const double2* __restrict__ col, int H, int F, int phase,
+                                       int bn, double count, double b_local,
+                                       const float* __restrict__ gamma,
+                                       const float* __restrict__ mean,
+                                       const float* __restrict__ rstd, double* acc,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       float* __restrict__ c123, const double* __restrict__ zsum,
+                                       float* __restrict__ db) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= F) return;
+  const int J = H / F;
+  if (!bn) {
+    for (int j = 0; j < J; ++j) db[j * F + ch] = (float)col[j * F + ch].x;
+    return;
+  }
+  double S1 = 0.0, S2 = 0.0;
+  if (phase <= 1) {
+    for (int j = 0; j < J; ++j) {
+      const double2 c = col[j * F + ch];
+      S1 += c.x;
+      S2 += c.y;
+    }
+    dgamma[ch] = (float)S2;
+    dbeta[ch] = (float)S1;
+    if (phase == 1) { acc[ch] = S1; acc[F + ch] = S2; return; }
+  } else {
+    S1 = acc[ch];
+    S2 = acc[F + ch];
+  }
+  const double rs = rstd[ch];
+  const double c1 = (double)gamma[ch] * rs;
+  const double c3 = -c1 * rs * S2 / count;
+  const double c2 = -c1 * S1 / count - c3 * (double)mean[ch];
+  c123[ch] = (float)c1;
+  c123[F + ch] = (float)c2;
+  c123[2 * F + ch] = (float)c3;
+  for (int j = 0; j < J; ++j) {
+    const int cj = j * F + ch;
+    db[cj] = (float)(c1 * col[cj].x + b_local * c2 + c3 * zsum[cj]);
+  }
+}
+
+void launch_bn_bwd_finalize(const double2* col, int H, int F, int phase, int bn, double count,
+                            double b_local, const float* gamma, const float* mean,
+                            const float* rstd, double* acc, float* dgamma, float* dbeta,
+                            float* c123, const double* zsum, float* db, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((F + 255) / 256), dim3(256), 0, s, col, H, F,
+                     phase, bn, count, b_local, gamma, mean, rstd, acc, dgamma, dbeta, c123, zsum,
+                     db);
+}
 
 __global__ __launch_bounds__(256) void bn_act_kernel(const float4* __restrict__ z,
                                                      const float4* __restrict__ res,
@@ -115,148 +191,10 @@ void launch_bn_act(const float* z, const float* res, float* h, const float* scal
                      (const float4*)res, (float4*)h, scale, shift, F, alpha, n4);
 }
 
-// One workgroup = kEwRows rows x one 64-column slab; lane = column.
-__global__ __launch_bounds__(256) void bnback_reduce_kernel(
-    const float* __restrict__ dh, const float* __restrict__ z, const float* __restrict__ scale,
-    const float* __restrict__ shift, const float* __restrict__ mean, const float* __restrict__ rstd,
-    int F, float alpha, int B, int H, float2* __restrict__ part) {
-  __shared__ float red[2][4][64];
-  const int nsl = H / 64;
-  const int rt = blockIdx.x / nsl, sl = blockIdx.x - rt * nsl;
-  const int t = threadIdx.x, f = t & 63, w = t >> 6;
-  const int col = sl * 64 + f, ch = col % F;
-  const float sc = scale[ch], sh = shift[ch], mu = mean[ch], rs = rstd[ch];
-  const int r0 = rt * kEwRows, r1 = min(B, r0 + kEwRows);
-  float s1 = 0.f, s2 = 0.f;
-  for (int r = r0 + w; r < r1; r += 4) {
-    const size_t o = (size_t)r * H + col;
-    const float zv = z[o], g = dh[o];
-    const float u = fmaf(zv, sc, sh);
-    const float du = u > 0.f ? g : g * alpha;
-    s1 += du;
-    s2 = fmaf(du, (zv - mu) * rs, s2);
-  }
-  red[0][w][f] = s1;
-  red[1][w][f] = s2;
-  __syncthreads();
-  if (w == 0) {
-    part[(size_t)rt * H + col] =
-        make_float2((red[0][0][f] + red[0][1][f]) + (red[0][2][f] + red[0][3][f]),
-                    (red[1][0][f] + red[1][1][f]) + (red[1][2][f] + red[1][3][f]));
-  }
-}
-
-void launch_bnback_reduce(const float* dh, const float* z, const float* scale, const float* shift,
-                          const float* mean, const float* rstd, int F, float alpha, int batch_norm,
-                          int B, int H, float2* part, hipStream_t s) {
-  (void)batch_norm;
-  const int grid = ((B + kEwRows - 1) / kEwRows) * (H / 64);
-  hipLaunchKernelGGL(bnback_reduce_kernel, dim3(grid), dim3(256), 0, s, dh, z, scale, shift, mean,
-                     rstd, F, alpha, B, H, part);
-}
-
-// c123 = [c1 | c2 | c3] (3F):  dz = c1*du + c2 + c3*z, with
-//   c1 = gamma*rstd, c3 = -c1*rstd*S2/N, c2 = -c1*S1/N - c3*mean,
-//   S1 = sum du = dbeta, S2 = sum du*zhat = dgamma   
-__global__ __launch_bounds__(256) void bnback_finalize_kernel(
-    const float2* __restrict__ part, int n_tiles, int H, int F, double count,
-    const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ rstd,
-    double* acc, int phase, float* dgamma, float* dbeta, float* c123) {
-  __shared__ double red[4];
-  const int ch = blockIdx.x;
-  const int J = H / F;
-  double S1, S2;
-  if (phase == 0 || phase == 1) {
-    double a1 = 0.0, a2 = 0.0;
-    const int n = n_tiles * J;
-    for (int e = threadIdx.x; e < n; e += 256) {
-      const int t = e / J, j = e - t * J;
-      const float2 p = part[(size_t)t * H + j * F + ch];
-      a1 += (double)p.x;
-      a2 += (double)p.y;
-    }
-    S1 = block_sum_d(a1, red);
-    S2 = block_sum_d(a2, red);
-    if (phase == 1) {
-      if (threadIdx.x == 0) { acc[ch] = S1; acc[F + ch] = S2; }
-      return;
-    }
-  } else {
-    S1 = acc[ch];
-    S2 = acc[F + ch];
-  }
-  if (threadIdx.x == 0) {
-    const double rs = rstd[ch];
-    const double c1 = (double)gamma[ch] * rs;
-    const double c3 = -c1 * rs * S2 / count;
-    const double c2 = -c1 * S1 / count - c3 * (double)mean[ch];
-    c123[ch] = (float)c1;
-    c123[F + ch] = (float)c2;
-    c123[2 * F + ch] = (float)c3;
-    dgamma[ch] = (float)S2;
-    dbeta[ch] = (float)S1;
-  }
-}
-
-void launch_bnback_finalize(const float2* part, int n_tiles, int H, int F, double count,
-                            const float* gamma, const float* mean, const float* rstd, double* acc,
-                            int phase, float* dgamma, float* dbeta, float* c123, hipStream_t s) {
-  hipLaunchKernelGGL(bnback_finalize_kernel, dim3(F), dim3(256), 0, s, part, n_tiles, H, F, count,
-                     gamma, mean, rstd, acc, phase, dgamma, dbeta, c123);
-}
-
-__global__ __launch_bounds__(256) void bnback_apply_kernel(
-    const float* __restrict__ dh, const float* __restrict__ z, const float* __restrict__ scale,
-    const float* __restrict__ shift, const float* __restrict__ c123, int F, float alpha, int B,
-    int H, float* __restrict__ dz, float* __restrict__ bpart) {
-  __shared__ float red[4][64];
-  const int nsl = H / 64;
-  const int rt = blockIdx.x / nsl, sl = blockIdx.x - rt * nsl;
-  const int t = threadIdx.x, f = t & 63, w = t >> 6;
-  const int col = sl * 64 + f, ch = col % F;
-  const float sc = scale[ch], sh = shift[ch];
-  const float c1 = c123[ch], c2 = c123[F + ch], c3 = c123[2 * F + ch];
-  const int r0 = rt * kEwRows, r1 = min(B, r0 + kEwRows);
-  float sb = 0.f;
-  for (int r = r0 + w; r < r1; r += 4) {
-    const size_t o = (size_t)r * H + col;
-    const float zv = z[o], g = dh[o];
-    const float u = fmaf(zv, sc, sh);
-    const float du = u > 0.f ? g : g * alpha;
-    const float d = fmaf(c1, du, fmaf(c3, zv, c2));
-    dz[o] = d;
-    sb += d;
-  }
-  red[w][f] = sb;
-  __syncthreads();
-  if (w == 0) bpart[(size_t)rt * H + col] = (red[0][f] + red[1][f]) + (red[2][f] + red[3][f]);
-}
-
-void launch_bnback_apply(const float* dh, const float* z, const float* scale, const float* shift,
-                         const float* c123, int F, float alpha, int batch_norm, int B, int H,
-                         float* dz, float* bpart, hipStream_t s) {
-  (void)batch_norm;
-  const int grid = ((B + kEwRows - 1) / kEwRows) * (H / 64);
-  hipLaunchKernelGGL(bnback_apply_kernel, dim3(grid), dim3(256), 0, s, dh, z, scale, shift, c123,
-                     F, alpha, B, H, dz, bpart);
-}
-
-__global__ void colsum_kernel(const float* __restrict__ part, int n_tiles, int H,
-                              float* __restrict__ out) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= H) return;
-  double s = 0.0;
-  for (int t = 0; t < n_tiles; ++t) s += (double)part[(size_t)t * H + col];
-  out[col] = (float)s;
-}
-
-void launch_colsum(const float* part, int n_tiles, int H, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(colsum_kernel, dim3((H + 255) / 256), dim3(256), 0, s, part, n_tiles, H, out);
-}
-
-// per-tile column sums of a narrow [B][ncols <= 64] matrix (the output bias gradient)
+// per-tile column sums of a narrow [B][ncols <= 64] matrix (the output bias
+// gradient), written as float2 (sum, 0) for colreduce
 __global__ __launch_bounds__(256) void colpart_kernel(const float* __restrict__ src, int B,
-                                                      int ncols, int ld, float* __restrict__ part) {
+                                                      int ncols, int ld, float2* __restrict__ part) {
   __shared__ float red[4][64];
   const int t = threadIdx.x, c = t & 63, w = t >> 6;
   const int r0 = blockIdx.x * kEwRows, r1 = min(B, r0 + kEwRows);
@@ -266,12 +204,22 @@ __global__ __launch_bounds__(256) void colpart_kernel(const float* __restrict__ 
   red[w][c] = s;
   __syncthreads();
   if (w == 0 && c < ncols)
-    part[(size_t)blockIdx.x * ncols + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    part[(size_t)blockIdx.x * ncols + c] =
+        make_float2((red[0][c] + red[1][c]) + (red[2][c] + red[3][c]), 0.f);
 }
 
-void launch_colpart(const float* src, int B, int ncols, int ld, float* part, hipStream_t s) {
+void launch_colpart(const float* src, int B, int ncols, int ld, float2* part, hipStream_t s) {
   hipLaunchKernelGGL(colpart_kernel, dim3((B + kEwRows - 1) / kEwRows), dim3(256), 0, s, src, B,
                      ncols, ld, part);
+}
+
+__global__ void col_to_float_kernel(const double2* __restrict__ col, int n, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (float)col[i].x;
+}
+
+void launch_col_to_float(const double2* col, int n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(col_to_float_kernel, dim3((n + 255) / 256), dim3(256), 0, s, col, n, out);
 }
 
 }  // namespace lcn

@@ -11,7 +11,12 @@ namespace lcn {
 // 4 waves in a 2x2 grid of 32x32 MFMA tiles; 64 batch rows per LDS stage.
 // Work ids are chunk-major so the blocks of one chunk (same batch rows) run
 // on one XCD and share A / dZ slabs through its L2.
-template <bool PRO>
+// PRO: A operand gets BN apply + LeakyReLU; DBB: the D operand is dz rebuilt
+// from (dh, z) by the BN + LeakyReLU backward, dz = c1 du + c2 + c3 z; the
+// workgroups of one designated block per output slab also store that dz
+// (dz_out) for the backward-data GEMM that follows, so dz costs one write and
+// no separate elementwise pass.
+template <bool PRO, bool DBB>
 __global__ __launch_bounds__(256) void gemm_dw_kernel(GemmDwArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* As = smem;            // [64 rows][64 p]
@@ -36,11 +41,17 @@ __global__ __launch_bounds__(256) void gemm_dw_kernel(GemmDwArgs a) {
     sc = *(const float4*)(a.pro_scale + ch);
     sh = *(const float4*)(a.pro_shift + ch);
   }
+  BnBackCoef dcf{};
+  if constexpr (DBB) {
+    const int ch = (sb.y % a.spj_in) * kSlab + 4 * c4;
+    dcf = load_bnback_coef(a.d_scale, a.d_shift, a.d_c123, a.d_F, ch);
+  }
   const float* asrc = a.A + (size_t)sb.x * kSlab + 4 * c4;
   const float* dsrc = a.D + (size_t)sb.y * kSlab + 4 * c4;
+  const float* zsrc = DBB ? a.d_z + (size_t)sb.y * kSlab + 4 * c4 : nullptr;
   const int glda = a.lda, gldd = a.ldd;
-  float4 ra0, ra1, ra2, ra3, rd0, rd1, rd2, rd3;
-  // rows >= r1 are clamped for the load and zeroed by a select (no branches)
+  float4 ra0, ra1, ra2, ra3, rd0, rd1, rd2, rd3, rz0, rz1, rz2, rz3;
+  // rows >= r1 are clamped for the load; their D operand is zeroed when staged
 #define DW_GLOAD(BASE)                                                              \
   {                                                                                 \
     const int q0_ = (BASE) + rr;                                                    \
@@ -54,11 +65,12 @@ __global__ __launch_bounds__(256) void gemm_dw_kernel(GemmDwArgs a) {
     rd1 = *(const float4*)(dsrc + (size_t)c1_ * gldd);                              \
     rd2 = *(const float4*)(dsrc + (size_t)c2_ * gldd);                              \
     rd3 = *(const float4*)(dsrc + (size_t)c3_ * gldd);                              \
-    const float z4 = 0.f;                                                           \
-    if (q0_ >= r1) rd0 = make_float4(z4, z4, z4, z4);                               \
-    if (q0_ + 16 >= r1) rd1 = make_float4(z4, z4, z4, z4);                          \
-    if (q0_ + 32 >= r1) rd2 = make_float4(z4, z4, z4, z4);                          \
-    if (q0_ + 48 >= r1) rd3 = make_float4(z4, z4, z4, z4);                          \
+    if constexpr (DBB) {                                                            \
+      rz0 = *(const float4*)(zsrc + (size_t)c0_ * gldd);                            \
+      rz1 = *(const float4*)(zsrc + (size_t)c1_ * gldd);                            \
+      rz2 = *(const float4*)(zsrc + (size_t)c2_ * gldd);                            \
+      rz3 = *(const float4*)(zsrc + (size_t)c3_ * gldd);                            \
+    }                                                                               \
   }
   if (r0 < r1) DW_GLOAD(r0);
   for (int base = r0; base < r1; base += 64) {
@@ -66,6 +78,28 @@ __global__ __launch_bounds__(256) void gemm_dw_kernel(GemmDwArgs a) {
     if constexpr (PRO) {
       ra0 = bnact4(ra0, sc, sh, a.alpha); ra1 = bnact4(ra1, sc, sh, a.alpha);
       ra2 = bnact4(ra2, sc, sh, a.alpha); ra3 = bnact4(ra3, sc, sh, a.alpha);
+    }
+    if constexpr (DBB) {  // D = dz rebuilt from (dh, z) of the layer
+      rd0 = bnback4(rd0, rz0, dcf, a.alpha); rd1 = bnback4(rd1, rz1, dcf, a.alpha);
+      rd2 = bnback4(rd2, rz2, dcf, a.alpha); rd3 = bnback4(rd3, rz3, dcf, a.alpha);
+    }
+    {
+      const int q0 = base + rr;
+      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (q0 >= r1) rd0 = z4;
+      if (q0 + 16 >= r1) rd1 = z4;
+      if (q0 + 32 >= r1) rd2 = z4;
+      if (q0 + 48 >= r1) rd3 = z4;
+    }
+    if constexpr (DBB) {  // one block per output slab writes dz for the dX GEMM
+      if (a.dz_out && a.dz_writer[b]) {
+        const int q0 = base + rr;
+        float* o = a.dz_out + (size_t)sb.y * kSlab + 4 * c4;
+        if (q0 < r1) *(float4*)(o + (size_t)q0 * gldd) = rd0;
+        if (q0 + 16 < r1) *(float4*)(o + (size_t)(q0 + 16) * gldd) = rd1;
+        if (q0 + 32 < r1) *(float4*)(o + (size_t)(q0 + 32) * gldd) = rd2;
+        if (q0 + 48 < r1) *(float4*)(o + (size_t)(q0 + 48) * gldd) = rd3;
+      }
     }
     {
       float* ad = As + rr * 64 + 4 * c4;
@@ -105,10 +139,15 @@ __global__ __launch_bounds__(256) void gemm_dw_kernel(GemmDwArgs a) {
 void launch_gemm_dw(const GemmDwArgs& a, hipStream_t s) {
   const int grid = a.nblk * a.nchunks;
   const size_t lds = 2 * 64 * 64 * sizeof(float);
-  if (a.pro_scale)
-    hipLaunchKernelGGL(gemm_dw_kernel<true>, dim3(grid), dim3(256), lds, s, a);
+  const bool pro = a.pro_scale != nullptr, dbb = a.d_bnback != 0;
+  if (pro && dbb)
+    hipLaunchKernelGGL((gemm_dw_kernel<true, true>), dim3(grid), dim3(256), lds, s, a);
+  else if (pro)
+    hipLaunchKernelGGL((gemm_dw_kernel<true, false>), dim3(grid), dim3(256), lds, s, a);
+  else if (dbb)
+    hipLaunchKernelGGL((gemm_dw_kernel<false, true>), dim3(grid), dim3(256), lds, s, a);
   else
-    hipLaunchKernelGGL(gemm_dw_kernel<false>, dim3(grid), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((gemm_dw_kernel<false, false>), dim3(grid), dim3(256), lds, s, a);
 }
 
 // Sum the chunk partials of every block in a fixed order and scatter into the

@@ -85,12 +85,18 @@ struct Handle {
   // x / y / dy of the thin layers are padded to 64 columns (pads stay zero)
   float *x = nullptr, *lab = nullptr, *out = nullptr, *dy = nullptr, *yout = nullptr;
   std::vector<float*> Z, Hb;
-  float *DH = nullptr, *DZ = nullptr, *DG = nullptr;
+  // DH: gradient w.r.t. a block output h_l; DG: w.r.t. the inner activation g;
+  // DZ: dz of a hidden layer, stored by its weight-gradient GEMM
+  float *DH = nullptr, *DG = nullptr, *DZ = nullptr;
+  int* dz_writer = nullptr;       // per hidden block: 1 for the first block of each output slab
   std::vector<BnStats> bn;
+  std::vector<double*> zsum;      // per BN layer: column sums of z (bias-gradient term)
   float *ident_scale = nullptr, *ident_shift = nullptr, *ident_c123 = nullptr;
   float* c123 = nullptr;
-  float2* stat_part = nullptr;
-  float *bpart = nullptr, *dw_part = nullptr, *col_part = nullptr;
+  float2* stat_part = nullptr;    // [B/128 tiles][H] GEMM epilogue partials
+  float2* col_part = nullptr;     // [B/kEwRows tiles][51] output-bias partials
+  double2* colacc = nullptr;      // [H] float64 column sums
+  float* dw_part = nullptr;
   double *loss_part = nullptr, *loss_sum = nullptr, *acc1 = nullptr, *acc2 = nullptr;
   int loss_grid = 1;
 
@@ -269,6 +275,10 @@ int build(Handle* h, const lcn_config* c) {
     bptr.push_back((int)bidx.size());
   }
   CHECK(upload(h, &h->blk, blk));
+  std::vector<int> writer(blk.size(), 0), seen(h->nslab, 0);
+  for (size_t b = 0; b < blk.size(); ++b)
+    if (!seen[blk[b].y]) { seen[blk[b].y] = 1; writer[b] = 1; }
+  CHECK(upload(h, &h->dz_writer, writer));
   CHECK(upload(h, &h->fwd_ptr, fptr));
   CHECK(upload(h, &h->bwd_ptr, bptr));
   CHECK(upload(h, &h->fwd_idx, fidx));
@@ -380,8 +390,10 @@ int build(Handle* h, const lcn_config* c) {
   h->Hb.assign(h->L + 1, nullptr);
   for (auto& hb : h->Hb) CHECK(dalloc(h, &hb, (size_t)B * H));
   CHECK(dalloc(h, &h->DH, (size_t)B * H));
-  CHECK(dalloc(h, &h->DZ, (size_t)B * H));
   CHECK(dalloc(h, &h->DG, (size_t)B * H));
+  CHECK(dalloc(h, &h->DZ, (size_t)B * H));
+  h->zsum.assign(nl - 1, nullptr);
+  for (auto& zs : h->zsum) CHECK(dalloc(h, &zs, (size_t)H));
   h->nbn = nl - 1;
   h->bn.resize(h->nbn);
   std::vector<float> ones(F, 1.f), zeros(F, 0.f), ic(3 * F, 0.f);
@@ -403,9 +415,9 @@ int build(Handle* h, const lcn_config* c) {
     }
   }
   CHECK(dalloc(h, &h->c123, 3 * F));
-  CHECK(dalloc(h, &h->stat_part, (size_t)cdiv(B, kMinTileRows) * H));
-  CHECK(dalloc(h, &h->bpart, (size_t)cdiv(B, kEwRows) * H));
+  CHECK(dalloc(h, &h->stat_part, (size_t)cdiv(B, kGemmBM) * H));
   CHECK(dalloc(h, &h->col_part, (size_t)cdiv(B, kEwRows) * 64));
+  CHECK(dalloc(h, &h->colacc, (size_t)H));
   h->loss_grid = (int)std::min<int64_t>(2048, cdiv(B, 4));
   CHECK(dalloc(h, &h->loss_part, (size_t)h->loss_grid));
   CHECK(dalloc(h, &h->loss_sum, 4));
@@ -451,57 +463,84 @@ int prep_weights(Handle* h) {
   return LCN_OK;
 }
 
-// BN statistics of linear layer k from partials with `tile` rows per tile
-int bn_stats(Handle* h, int k, int B, int tile) {
+// BN statistics of BN layer k from the EPI_BNFWD partials its GEMM wrote
+// (one SyncBN all-reduce of 2F doubles with several GPUs); also keeps the
+// column sums of z for the bias gradient of the backward
+int bn_stats(Handle* h, int k, int B) {
   if (!h->batch_norm) return LCN_OK;
   hipStream_t s = h->stream;
   const double count = (double)B * h->world * kJ;
   const float* gamma = h->theta + h->gamma_off[k];
   const float* beta = h->theta + h->beta_off[k];
-  const int nt = (int)cdiv(B, tile);
+  launch_colreduce(h->stat_part, (int)cdiv(B, kGemmBM), kGemmBM, B, h->H, 1, h->colacc, s);
   if (h->world == 1) {
-    launch_bn_finalize(h->stat_part, nt, tile, B, h->H, h->F, gamma, beta, h->eps, count, h->acc1,
-                       h->acc2, 0, h->bn[k], s);
+    launch_bn_fwd_finalize(h->colacc, h->H, h->F, 0, count, gamma, beta, h->eps, h->acc1, h->bn[k],
+                           h->zsum[k], s);
     return LCN_OK;
   }
-  launch_bn_finalize(h->stat_part, nt, tile, B, h->H, h->F, gamma, beta, h->eps, count, h->acc1,
-                     h->acc2, 1, h->bn[k], s);
-  CHECK(allreduce(h, h->acc1, h->F, ncclDouble));
-  launch_bn_finalize(h->stat_part, nt, tile, B, h->H, h->F, gamma, beta, h->eps, count, h->acc1,
-                     h->acc2, 2, h->bn[k], s);
-  CHECK(allreduce(h, h->acc2, h->F, ncclDouble));
-  launch_bn_finalize(h->stat_part, nt, tile, B, h->H, h->F, gamma, beta, h->eps, count, h->acc1,
-                     h->acc2, 3, h->bn[k], s);
+  launch_bn_fwd_finalize(h->colacc, h->H, h->F, 1, count, gamma, beta, h->eps, h->acc1, h->bn[k],
+                         h->zsum[k], s);
+  CHECK(allreduce(h, h->acc1, 2 * h->F, ncclDouble));
+  launch_bn_fwd_finalize(h->colacc, h->H, h->F, 2, count, gamma, beta, h->eps, h->acc1, h->bn[k],
+                         nullptr, s);
   return LCN_OK;
 }
 
+// A GEMM operand: a [B][ld] tensor, read as is (PRO_RAW), through BN apply +
+// LeakyReLU of BN layer `layer` (PRO_BNACT: p = z of that layer), or as the dz
+// of BN layer `layer` rebuilt from p = dh and its z (PRO_BNBACK).
+struct Operand {
+  const float* p; int ld;
+  int mode; int layer;
+};
+Operand raw(const float* p, int ld) { return Operand{p, ld, PRO_RAW, -1}; }
+
 // One launch of the block-sparse MFMA GEMM: Y[:, so-slab] = sum over the CSR
-// list of X[:, si-slab] . block (+ bias / + addsrc), optional BN prologue on X
-// and BN partials in the epilogue.  `timer` < 0: not timed.
+// list of X[:, si-slab] . block (+ bias / + addsrc); epilogue partials:
+// EPI_BNFWD (BN statistics of Y) or EPI_BNBACK for BN layer `epi_layer`.
+// `timer` < 0: not timed.
 struct GemmCall {
-  const float* X; int ldx;
+  Operand X;
   const float* blocks; const int* ptr; const int2* idx; int n_out_slabs;
-  const float* bias; const BnStats* pro;
-  float* Y; int ldy; const float* addsrc; bool stats;
+  const float* bias;
+  float* Y; int ldy; const float* addsrc;
+  int epi_mode; int epi_layer;
   int timer; double flops_per_row;
 };
 
 int gemm(Handle* h, const GemmCall& c, int B) {
+  if (c.X.mode == PRO_BNBACK) {
+    h->err = "internal: the block-sparse GEMM takes a stored dz (PRO_BNBACK is dW-only)";
+    return LCN_E_ARG;
+  }
   GemmArgs a{};
-  a.X = c.X;
-  a.ldx = c.ldx;
+  a.X = c.X.p;
+  a.ldx = c.X.ld;
   a.blocks = c.blocks;
   a.ptr = c.ptr;
   a.idx = c.idx;
   a.bias = c.bias;
-  a.pro_scale = c.pro ? c.pro->scale : nullptr;
-  a.pro_shift = c.pro ? c.pro->shift : nullptr;
+  a.pro_mode = c.X.mode;
+  if (c.X.mode == PRO_BNACT) {
+    a.pro_scale = h->bn[c.X.layer].scale;
+    a.pro_shift = h->bn[c.X.layer].shift;
+  }
   a.spj_in = h->spj;
   a.alpha = h->alpha;
   a.Y = c.Y;
   a.ldy = c.ldy;
   a.addsrc = c.addsrc;
-  a.stat = c.stats ? h->stat_part : nullptr;
+  a.epi_mode = c.epi_mode;
+  a.stat = c.epi_mode != EPI_NONE ? h->stat_part : nullptr;
+  if (c.epi_mode == EPI_BNBACK) {
+    const BnStats& st = h->bn[c.epi_layer];
+    a.epi_z = h->Z[c.epi_layer];
+    a.epi_scale = st.scale;
+    a.epi_shift = st.shift;
+    a.epi_mean = st.mean;
+    a.epi_rstd = st.rstd;
+  }
+  a.epi_F = h->F;
   a.B = B;
   a.n_out_slabs = c.n_out_slabs;
   a.variant = h->gemm_variant;
@@ -514,29 +553,47 @@ int gemm(Handle* h, const GemmCall& c, int B) {
 }
 
 // hidden layer k: forward (kindt = LCN_K_GEMM_FWD) or backward-data (LCN_K_GEMM_DX)
-int gemm_hidden(Handle* h, int k, int kindt, const float* X, const BnStats* pro, float* Y,
-                const float* addsrc, bool stats, int B) {
+int gemm_hidden(Handle* h, int k, int kindt, const Operand& X, float* Y, const float* addsrc,
+                int epi_mode, int epi_layer, int B) {
   const WLayer& Lr = h->wl[k];
   const bool fwd = kindt == LCN_K_GEMM_FWD;
-  GemmCall c{X, h->H, fwd ? Lr.blk_fwd : Lr.blk_bwd, fwd ? h->fwd_ptr : h->bwd_ptr,
+  GemmCall c{X, fwd ? Lr.blk_fwd : Lr.blk_bwd, fwd ? h->fwd_ptr : h->bwd_ptr,
              fwd ? h->fwd_idx : h->bwd_idx, h->nslab, fwd ? h->theta + h->b_off[k] : nullptr,
-             pro, Y, h->H, addsrc, stats, kindt, 2.0 * 4096.0 * h->nblk};  // 2*64*64 per block
+             Y, h->H, addsrc, epi_mode, epi_layer,
+             kindt, 2.0 * 4096.0 * h->nblk};  // 2*64*64 FLOP per block per row
   return gemm(h, c, B);
 }
 
-// dW_e of a layer from A (input activations, optional BN prologue) and D (dZ):
-// partial slabs per batch chunk, then a fixed-order reduce into the raw-gradient
-// vector (rows / columns past the valid range are padding and are dropped)
-int gemm_dw(Handle* h, const float* A, int lda, const BnStats* pro, const float* D, int ldd,
-            const int2* blk, int nblk, float* dW, int ld, int rows_valid, int cols_valid,
-            int B, bool timed) {
+// dW_e of a layer from A (input activations, raw or BN-apply prologue) and D
+// (raw, or dz rebuilt from (dh, z) by the BN backward prologue -- then also
+// stored to dz_out when given): partial slabs per batch chunk, then a
+// fixed-order reduce into the raw-gradient vector (rows / columns past the
+// valid range are padding and are dropped)
+int gemm_dw(Handle* h, const Operand& A, const Operand& D, const int2* blk, int nblk, float* dW,
+            int ld, int rows_valid, int cols_valid, int B, bool timed, float* dz_out = nullptr) {
   GemmDwArgs a{};
-  a.A = A;
-  a.lda = lda;
-  a.D = D;
-  a.ldd = ldd;
-  a.pro_scale = pro ? pro->scale : nullptr;
-  a.pro_shift = pro ? pro->shift : nullptr;
+  a.A = A.p;
+  a.lda = A.ld;
+  a.D = D.p;
+  a.ldd = D.ld;
+  if (A.mode == PRO_BNACT) {
+    a.pro_scale = h->bn[A.layer].scale;
+    a.pro_shift = h->bn[A.layer].shift;
+  }
+  if (D.mode == PRO_BNBACK) {
+    a.d_bnback = 1;
+    a.d_scale = h->bn[D.layer].scale;
+    a.d_shift = h->bn[D.layer].shift;
+    a.d_z = h->Z[D.layer];
+    a.d_c123 = h->batch_norm ? h->c123 : h->ident_c123;
+    a.d_F = h->F;
+    a.dz_out = dz_out;
+    a.dz_writer = h->dz_writer;
+    if (dz_out && blk != h->blk) {
+      h->err = "internal: dz store needs the hidden block list";
+      return LCN_E_ARG;
+    }
+  }
   a.spj_in = h->spj;
   a.alpha = h->alpha;
   a.blk = blk;
@@ -554,35 +611,30 @@ int gemm_dw(Handle* h, const float* A, int lda, const BnStats* pro, const float*
   return LCN_OK;
 }
 
-// dz of linear layer k from the incoming gradient dh (w.r.t. the layer's
-// activation output); writes DZ, the BN parameter grads and the bias grad.
-int bn_back(Handle* h, int k, const float* dh, int B) {
+// BN + LeakyReLU backward of BN layer k from the EPI_BNBACK partials (sum du,
+// sum du*zhat) the GEMM producing its incoming gradient wrote: the dz
+// coefficients c123 (consumed by the PRO_BNBACK prologues), the BN parameter
+// grads and the bias grad.  dz itself is never materialised.
+int bn_back(Handle* h, int k, int B) {
   hipStream_t s = h->stream;
   const BnStats& st = h->bn[k];
-  const float* c123 = h->ident_c123;
-  if (h->batch_norm) {
-    const int nt = (int)cdiv(B, kEwRows);
-    const double count = (double)B * h->world * kJ;
-    launch_bnback_reduce(dh, h->Z[k], st.scale, st.shift, st.mean, st.rstd, h->F, h->alpha, 1, B,
-                         h->H, h->stat_part, s);
-    const float* gamma = h->theta + h->gamma_off[k];
-    float* dgam = h->rg + h->gamma_off[k];
-    float* dbet = h->rg + h->beta_off[k];
-    if (h->world == 1) {
-      launch_bnback_finalize(h->stat_part, nt, h->H, h->F, count, gamma, st.mean, st.rstd, h->acc1,
-                             0, dgam, dbet, h->c123, s);
-    } else {
-      launch_bnback_finalize(h->stat_part, nt, h->H, h->F, count, gamma, st.mean, st.rstd, h->acc1,
-                             1, dgam, dbet, h->c123, s);
-      CHECK(allreduce(h, h->acc1, 2 * h->F, ncclDouble));
-      launch_bnback_finalize(h->stat_part, nt, h->H, h->F, count, gamma, st.mean, st.rstd, h->acc1,
-                             2, dgam, dbet, h->c123, s);
-    }
-    c123 = h->c123;
+  const int bn = h->batch_norm;
+  const double count = (double)B * h->world * kJ;
+  const float* gamma = bn ? h->theta + h->gamma_off[k] : nullptr;
+  float* dgam = bn ? h->rg + h->gamma_off[k] : nullptr;
+  float* dbet = bn ? h->rg + h->beta_off[k] : nullptr;
+  float* db = h->rg + h->b_off[k];
+  launch_colreduce(h->stat_part, (int)cdiv(B, kGemmBM), kGemmBM, B, h->H, 0, h->colacc, s);
+  if (h->world == 1 || !bn) {
+    launch_bn_bwd_finalize(h->colacc, h->H, h->F, 0, bn, count, (double)B, gamma, st.mean, st.rstd,
+                           h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
+    return LCN_OK;
   }
-  launch_bnback_apply(dh, h->Z[k], st.scale, st.shift, c123, h->F, h->alpha, h->batch_norm, B, h->H,
-                      h->DZ, h->bpart, s);
-  launch_colsum(h->bpart, (int)cdiv(B, kEwRows), h->H, h->rg + h->b_off[k], s);
+  launch_bn_bwd_finalize(h->colacc, h->H, h->F, 1, bn, count, (double)B, gamma, st.mean, st.rstd,
+                         h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
+  CHECK(allreduce(h, h->acc1, 2 * h->F, ncclDouble));
+  launch_bn_bwd_finalize(h->colacc, h->H, h->F, 2, bn, count, (double)B, gamma, st.mean, st.rstd,
+                         h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
   return LCN_OK;
 }
 
@@ -590,29 +642,28 @@ int forward(Handle* h, int B, bool with_labels, bool train) {
   hipStream_t s = h->stream;
   const int H = h->H, nl = h->nl;
   CHECK(prep_weights(h));
-  const int tile = gemm_bs_rows(h->gemm_variant);
+  const int epi = h->batch_norm ? EPI_BNFWD : EPI_NONE;
   // lift z0 = x . W1e + b1 (models_att.py:714-729): x padded to one 64-wide slab
   const double thin_flops = 2.0 * 4096.0 * h->nslab;
-  CHECK(gemm(h, GemmCall{h->x, 64, h->wl[0].blk_fwd, h->thin_ptr, h->thin_idx, h->nslab,
-                         h->theta + h->b_off[0], nullptr, h->Z[0], H, nullptr,
-                         (bool)h->batch_norm, -1, thin_flops}, B));
-  CHECK(bn_stats(h, 0, B, tile));
+  CHECK(gemm(h, GemmCall{raw(h->x, 64), h->wl[0].blk_fwd, h->thin_ptr, h->thin_idx, h->nslab,
+                         h->theta + h->b_off[0], h->Z[0], H, nullptr, epi, -1, -1, thin_flops}, B));
+  CHECK(bn_stats(h, 0, B));
   launch_bn_act(h->Z[0], nullptr, h->Hb[0], h->bn[0].scale, h->bn[0].shift, h->F, h->alpha, B, H, s);
   // two_linear blocks (models_att.py:630-705)
   for (int l = 0; l < h->L; ++l) {
     const int k1 = 2 * l + 1, k2 = 2 * l + 2;
-    CHECK(gemm_hidden(h, k1, LCN_K_GEMM_FWD, h->Hb[l], nullptr, h->Z[k1], nullptr, h->batch_norm, B));
-    CHECK(bn_stats(h, k1, B, tile));
-    CHECK(gemm_hidden(h, k2, LCN_K_GEMM_FWD, h->Z[k1], &h->bn[k1], h->Z[k2], nullptr,
-                      h->batch_norm, B));
-    CHECK(bn_stats(h, k2, B, tile));
+    CHECK(gemm_hidden(h, k1, LCN_K_GEMM_FWD, raw(h->Hb[l], H), h->Z[k1], nullptr, epi, -1, B));
+    CHECK(bn_stats(h, k1, B));
+    CHECK(gemm_hidden(h, k2, LCN_K_GEMM_FWD, Operand{h->Z[k1], H, PRO_BNACT, k1}, h->Z[k2],
+                      nullptr, epi, -1, B));
+    CHECK(bn_stats(h, k2, B));
     launch_bn_act(h->Z[k2], h->residual ? h->Hb[l] : nullptr, h->Hb[l + 1], h->bn[k2].scale,
                   h->bn[k2].shift, h->F, h->alpha, B, H, s);
   }
   // output layer y = h_L . W4e + b4 into a [B][64] buffer (51 used), then the
   // output assembly, loss and d out (models_att.py:749-773, :356)
-  CHECK(gemm(h, GemmCall{h->Hb[h->L], H, h->wl[nl - 1].blk_fwd, h->out_ptr, h->out_idx, 1,
-                         nullptr, nullptr, h->yout, 64, nullptr, false, -1, thin_flops}, B));
+  CHECK(gemm(h, GemmCall{raw(h->Hb[h->L], H), h->wl[nl - 1].blk_fwd, h->out_ptr, h->out_idx, 1,
+                         nullptr, h->yout, 64, nullptr, EPI_NONE, -1, -1, thin_flops}, B));
   OutAsmArgs oa{};
   oa.y = h->yout;
   oa.b4 = h->theta + h->b_off[nl - 1];
@@ -635,31 +686,41 @@ int backward(Handle* h, int B) {
   const int nl = h->nl, L = h->L;
   const int H = h->H;
   const WLayer& Lo = h->wl[nl - 1];
+  // Every dX GEMM stores the incoming gradient dh of the BN layer below it and
+  // its epilogue reduces that layer's (sum du, sum du*zhat); bn_back turns
+  // them into c123; the layer's dW GEMM rebuilds dz = c1 du + c2 + c3 z while
+  // staging its D operand and stores it (DZ) for the layer's dX GEMM.
   // output layer: dh_L = dy . W4e^T (dy padded to 64 columns), dW4e = h_L^T dy, db4 = sum dy
-  CHECK(gemm(h, GemmCall{h->dy, 64, Lo.blk_bwd, h->thin_ptr, h->thin_idx, h->nslab, nullptr,
-                         nullptr, h->DH, H, nullptr, false, -1, 0.0}, B));
-  CHECK(gemm_dw(h, h->Hb[L], H, nullptr, h->dy, 64, h->out_blk, h->nslab, h->rg + Lo.w_off, 51,
+  const int top = nl - 2;  // BN layer under the output layer
+  CHECK(gemm(h, GemmCall{raw(h->dy, 64), Lo.blk_bwd, h->thin_ptr, h->thin_idx, h->nslab, nullptr,
+                         h->DH, H, nullptr, EPI_BNBACK, top, -1, 0.0}, B));
+  CHECK(gemm_dw(h, raw(h->Hb[L], H), raw(h->dy, 64), h->out_blk, h->nslab, h->rg + Lo.w_off, 51,
                 H, 51, B, false));
+  const int ct = (int)cdiv(B, kEwRows);
   launch_colpart(h->dy, B, 51, 64, h->col_part, s);
-  launch_colsum(h->col_part, (int)cdiv(B, kEwRows), 51, h->rg + h->b_off[nl - 1], s);
+  launch_colreduce(h->col_part, ct, kEwRows, B, 51, 0, h->colacc, s);
+  launch_col_to_float(h->colacc, 51, h->rg + h->b_off[nl - 1], s);
 
   for (int l = L - 1; l >= 0; --l) {
     const int k1 = 2 * l + 1, k2 = 2 * l + 2;
+    const int below = l > 0 ? k1 - 1 : 0;  // BN layer under block l's input h_l
     // DH = dh_{l+1}: gradient of the block output
-    CHECK(bn_back(h, k2, h->DH, B));                                   // DZ = dz_k2
-    CHECK(gemm_dw(h, h->Z[k1], H, &h->bn[k1], h->DZ, H, h->blk, h->nblk,
-                  h->rg + h->wl[k2].w_off, H, H, H, B, true));         // dW_k2 = g^T dz
-    CHECK(gemm_hidden(h, k2, LCN_K_GEMM_DX, h->DZ, nullptr, h->DG, nullptr, false, B));  // dg
-    CHECK(bn_back(h, k1, h->DG, B));                                   // DZ = dz_k1
-    CHECK(gemm_dw(h, h->Hb[l], H, nullptr, h->DZ, H, h->blk, h->nblk,
-                  h->rg + h->wl[k1].w_off, H, H, H, B, true));         // dW_k1 = h_l^T dz
-    CHECK(gemm_hidden(h, k1, LCN_K_GEMM_DX, h->DZ, nullptr, h->DH,
-                      h->residual ? h->DH : nullptr, false, B));       // dh_l (+ residual)
+    CHECK(bn_back(h, k2, B));
+    CHECK(gemm_dw(h, Operand{h->Z[k1], H, PRO_BNACT, k1}, Operand{h->DH, H, PRO_BNBACK, k2},
+                  h->blk, h->nblk, h->rg + h->wl[k2].w_off, H, H, H, B, true,
+                  h->DZ));                                             // dW_k2 = g^T dz2; DZ = dz2
+    CHECK(gemm_hidden(h, k2, LCN_K_GEMM_DX, raw(h->DZ, H), h->DG, nullptr, EPI_BNBACK, k1, B));
+    CHECK(bn_back(h, k1, B));
+    CHECK(gemm_dw(h, raw(h->Hb[l], H), Operand{h->DG, H, PRO_BNBACK, k1}, h->blk, h->nblk,
+                  h->rg + h->wl[k1].w_off, H, H, H, B, true,
+                  h->DZ));                                             // dW_k1 = h_l^T dz1; DZ = dz1
+    CHECK(gemm_hidden(h, k1, LCN_K_GEMM_DX, raw(h->DZ, H), h->DH, h->residual ? h->DH : nullptr,
+                      EPI_BNBACK, below, B));                          // dh_l (+ residual)
   }
   // lift: dz0, dW1e = x^T dz0 (x padded: rows >= 17*in_F dropped), db1
-  CHECK(bn_back(h, 0, h->DH, B));
-  CHECK(gemm_dw(h, h->x, 64, nullptr, h->DZ, H, h->lift_blk, h->nslab, h->rg + h->wl[0].w_off, H,
-                kJ * h->inF, H, B, false));
+  CHECK(bn_back(h, 0, B));
+  CHECK(gemm_dw(h, raw(h->x, 64), Operand{h->DH, H, PRO_BNBACK, 0}, h->lift_blk, h->nslab,
+                h->rg + h->wl[0].w_off, H, kJ * h->inF, H, B, false));
   return LCN_OK;
 }
 

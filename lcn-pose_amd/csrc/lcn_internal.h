@@ -9,29 +9,40 @@ namespace lcn {
 constexpr int kJ = 17;          // joints (models_att.py:512-513)
 constexpr int kSlab = 64;       // feature slab = MFMA tile edge; F is a multiple of it
 constexpr int kGemmBM = 128;    // batch rows per block-sparse GEMM tile
-constexpr int kMinTileRows = 64;  // smallest GEMM row tile (sizes the BN partial buffers)
-constexpr int kEwRows = 256;    // rows per tile of the BN-backward elementwise kernels
+constexpr int kEwRows = 256;    // rows per tile of the output-bias column partials
 
 // ----------------------------------------------------------------------------
 // Block-sparse GEMM (forward z = a.We + b and backward dA = dZ.We^T).
 // Output slab `so` of a row tile accumulates X[:, si-slab] . blocks[blk] over
 // the (si, blk) list ptr[so]..ptr[so+1].  Blocks are 64x64, [n][k] (k fastest).
 // ----------------------------------------------------------------------------
+// operand transform applied while staging: raw, BN apply + LeakyReLU, or (the
+// weight-gradient kernel's D operand) the BN + LeakyReLU backward dz from dh, z
+enum { PRO_RAW = 0, PRO_BNACT = 1, PRO_BNBACK = 2 };
+// epilogue partials: EPI_BNFWD = BN statistics of the output (sum, M2 about the
+// tile mean); EPI_BNBACK = BN-backward sums of the layer below (sum du, sum du*zhat)
+enum { EPI_NONE = 0, EPI_BNFWD = 1, EPI_BNBACK = 2 };
+
 struct GemmArgs {
   const float* X; int ldx;           // A operand source [B][ldx]
   const float* blocks;               // packed blocks
   const int* ptr;                    // [n_out_slabs + 1]
   const int2* idx;                   // (in_slab, block id)
   const float* bias;                 // [n_out_slabs*64] or null
-  const float* pro_scale;            // prologue BN scale per input channel, or null (raw)
+  int pro_mode;                      // PRO_RAW or PRO_BNACT
+  const float* pro_scale;            // forward BN scale / shift of the input's layer
   const float* pro_shift;
   int spj_in;                        // input slabs per joint (channel = (si % spj)*64 + k)
-  float alpha;                       // LeakyReLU slope of the prologue
+  float alpha;                       // LeakyReLU slope
   float* Y; int ldy;                 // output [B][ldy]
   const float* addsrc;               // Y = acc (+ addsrc) ; may alias Y
-  float2* stat;                      // BN partials [row_tiles][ldy] (sum, m2) or null
+  int epi_mode;
+  float2* stat;                      // partials [row_tiles][ldy]
+  const float* epi_z;                // EPI_BNBACK: z of the layer below [B][ldy]
+  const float* epi_scale; const float* epi_shift; const float* epi_mean; const float* epi_rstd;
+  int epi_F;
   int B; int n_out_slabs; int n_row_tiles;
-  int variant;                       // tile / pipeline variant (kernels_gemm.hip)
+  int variant;                       // reserved (tile variant)
 };
 void launch_gemm_bs(const GemmArgs& a, hipStream_t s);
 int gemm_bs_rows(int variant);       // batch rows per workgroup tile of a variant
@@ -39,8 +50,12 @@ int gemm_bs_rows(int variant);       // batch rows per workgroup tile of a varia
 // dWe blocks: part[chunk][blk][p][q] = sum_{b in chunk} A[b, si*64+p] * D[b, so*64+q]
 struct GemmDwArgs {
   const float* A; int lda;
-  const float* D; int ldd;
-  const float* pro_scale; const float* pro_shift; int spj_in; float alpha;
+  const float* D; int ldd;           // d_bnback: D = dh and the operand is dz (PRO_BNBACK)
+  const float* pro_scale; const float* pro_shift; int spj_in; float alpha;  // A: BN apply + act
+  int d_bnback;
+  const float* d_z; const float* d_scale; const float* d_shift; const float* d_c123; int d_F;
+  const int* dz_writer;              // D_BNBACK: per block, 1 if it stores dz (one per so)
+  float* dz_out;                     // D_BNBACK: dz [B][ldd] or null
   const int2* blk;                   // (si, so) per block
   int nblk;
   int B; int chunk_rows; int nchunks;
@@ -77,32 +92,29 @@ void launch_out_assemble(const OutAsmArgs& a, int grid, hipStream_t s);
 // ----------------------------------------------------------------------------
 // stats per channel: mean, rstd, scale = gamma*rstd, shift = beta - mean*scale
 struct BnStats { float* mean; float* rstd; float* scale; float* shift; };
-// phase 0: complete (single GPU); 1: local s1 -> acc[F]; 2: s2 about mean(acc_s1) -> acc2;
-// 3: final from acc1/acc2.  count = rows_global * J.
-void launch_bn_finalize(const float2* part, int n_row_tiles, int tile_rows, int B, int H, int F,
-                        const float* gamma, const float* beta, float eps, double count,
-                        double* acc1, double* acc2, int phase, BnStats st, hipStream_t s);
+// float64 column sums of tile partials part[n_tiles][H]:
+//   mode 0 (sum x, sum y); mode 1 (sum x, sum (y + x^2 / rows_of_tile))
+void launch_colreduce(const float2* part, int n_tiles, int tile_rows, int B, int H, int mode,
+                      double2* out, hipStream_t s);
+// forward BN finish from colreduce mode-1 sums.  phase 0 complete (single GPU);
+// 1 local channel sums -> acc[2F]; 2 finish from all-reduced acc.  count =
+// rows_global * J.  zsum (optional): per-column sum of z.
+void launch_bn_fwd_finalize(const double2* col, int H, int F, int phase, double count,
+                            const float* gamma, const float* beta, float eps, double* acc,
+                            BnStats st, double* zsum, hipStream_t s);
+// backward BN finish from colreduce mode-0 sums of (du, du*zhat): c1|c2|c3,
+// local dgamma/dbeta and the bias gradient db; bn = 0: db = sum du only
+void launch_bn_bwd_finalize(const double2* col, int H, int F, int phase, int bn, double count,
+                            double b_local, const float* gamma, const float* mean,
+                            const float* rstd, double* acc, float* dgamma, float* dbeta,
+                            float* c123, const double* zsum, float* db, hipStream_t s);
 // h = [res +] leaky(scale*z + shift)
 void launch_bn_act(const float* z, const float* res, float* h, const float* scale,
                    const float* shift, int F, float alpha, int B, int H, hipStream_t s);
-// partial (sum du, sum du*zhat) per [B/256 tile][H]; du = dh * leaky'(u)
-void launch_bnback_reduce(const float* dh, const float* z, const float* scale,
-                          const float* shift, const float* mean, const float* rstd, int F,
-                          float alpha, int batch_norm, int B, int H, float2* part, hipStream_t s);
-// phase 0 complete; 1 local sums -> acc (2F doubles); 2 finish from acc.
-// writes dgamma/dbeta (into the raw-grad buffer) and c1,c2,c3
-void launch_bnback_finalize(const float2* part, int n_tiles, int H, int F, double count,
-                            const float* gamma, const float* mean, const float* rstd,
-                            double* acc, int phase, float* dgamma, float* dbeta, float* c123,
-                            hipStream_t s);
-// dz = c1*du + c2 + c3*z ; per-tile column sums of dz -> bpart[tile][H]
-void launch_bnback_apply(const float* dh, const float* z, const float* scale,
-                         const float* shift, const float* c123, int F, float alpha,
-                         int batch_norm, int B, int H, float* dz, float* bpart, hipStream_t s);
-// db[col] = sum_tiles bpart[tile][col]
-void launch_colsum(const float* part, int n_tiles, int H, float* out, hipStream_t s);
-// per-kEwRows-tile column sums of src[B][ncols] (ncols <= 64) -> part[tiles][ncols]
-void launch_colpart(const float* src, int B, int ncols, int ld, float* part, hipStream_t s);
+// per-kEwRows-tile column sums of src[B][ncols] (ncols <= 64) -> part[tiles][ncols] as (sum, 0)
+void launch_colpart(const float* src, int B, int ncols, int ld, float2* part, hipStream_t s);
+// out[i] = (float) col[i].x
+void launch_col_to_float(const double2* col, int n, float* out, hipStream_t s);
 void launch_loss_finalize(const double* part, int n, double* out, hipStream_t s);
 
 // ----------------------------------------------------------------------------
