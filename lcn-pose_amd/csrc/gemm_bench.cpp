@@ -5,6 +5,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <random>
 #include <vector>
@@ -100,7 +101,7 @@ int main(int argc, char** argv) {
   float* Y;
   CK(hipMalloc(&Y, (size_t)B * H * 4));
   float2* stat;
-  CK(hipMalloc(&stat, (size_t)(B / 128 + 1) * H * 8));
+  CK(hipMalloc(&stat, (size_t)(B / 32 + 1) * H * 8));
   const int nch = std::max(1, std::min(64, 8192 / nblk));
   float* part;
   CK(hipMalloc(&part, (size_t)nch * nblk * 4096 * 4));
@@ -114,11 +115,13 @@ int main(int argc, char** argv) {
   const double flop = 2.0 * 4096.0 * nblk * B;
 
   // kind 0: forward (bias, EPI_BNFWD); 1: backward-data (+residual, EPI_BNBACK)
+  // kind 3: forward without epilogue partials; 4: same with every row reading
+  // row 0 of X (ldx = 0: operand traffic all cache hits -- the in-core ceiling)
   auto mk = [&](int kind, int pro, int variant) {
-    const bool fwd = kind == 0;
+    const bool fwd = kind == 0 || kind >= 3;
     GemmArgs a{};
     a.X = X;
-    a.ldx = H;
+    a.S_in = kind == 4 ? 0 : J;
     a.blocks = W;
     a.ptr = fwd ? dfp : dbp;
     a.idx = fwd ? dfi : dbi;
@@ -126,12 +129,13 @@ int main(int argc, char** argv) {
     a.pro_mode = pro;
     a.pro_scale = pro ? sc : nullptr;
     a.pro_shift = pro ? sh : nullptr;
+    a.pro_F = F;
     a.spj_in = 1;
     a.alpha = 0.2f;
     a.Y = Y;
-    a.ldy = H;
+    a.S_out = J;
     a.addsrc = fwd ? nullptr : Y;
-    a.epi_mode = fwd ? EPI_BNFWD : EPI_BNBACK;
+    a.epi_mode = kind >= 3 ? EPI_NONE : fwd ? EPI_BNFWD : EPI_BNBACK;
     a.stat = stat;
     a.epi_z = X2;
     a.epi_scale = sc;
@@ -141,16 +145,17 @@ int main(int argc, char** argv) {
     a.epi_F = F;
     a.B = B;
     a.n_out_slabs = J;
-    a.variant = variant;
-    a.n_row_tiles = (B + gemm_bs_rows(variant) - 1) / gemm_bs_rows(variant);
+    a.n_rt = (B + kRT - 1) / kRT;
+    (void)variant;
     return a;
   };
   GemmDwArgs d{};
   d.A = X;
-  d.lda = H;
+  d.S_a = J;
   d.D = X2;
-  d.ldd = H;
-  d.spj_in = 1;
+  d.S_d = J;
+  d.spj_a = 1;
+  d.spj_d = 1;
   d.alpha = 0.2f;
   d.d_z = X;
   d.d_scale = sc;
@@ -178,11 +183,19 @@ int main(int argc, char** argv) {
     cases.push_back({"fwd raw +bnstat", 0, PRO_RAW, v});
     cases.push_back({"fwd bnact +bnstat", 0, PRO_BNACT, v});
     cases.push_back({"dx raw +bnback", 1, PRO_RAW, v});
+    cases.push_back({"fwd raw no-epi", 3, PRO_RAW, v});
+    cases.push_back({"fwd raw no-epi hotX", 4, PRO_RAW, v});
   }
   cases.push_back({"dw raw", 2, PRO_RAW, 0});
   cases.push_back({"dw bnact x bnback", 2, PRO_BNACT, 0});
   cases.push_back({"dw raw x bnback", 2, PRO_BNBACK, 0});
-  const int rounds = 3;
+  if (argc > 5) {  // keep only the cases whose name contains argv[5]
+    std::vector<Case> keep;
+    for (const Case& c : cases)
+      if (std::strstr(c.name, argv[5])) keep.push_back(c);
+    cases.swap(keep);
+  }
+  const int rounds = argc > 6 ? std::atoi(argv[6]) : 3;
   for (int r = 0; r < rounds; ++r) {
     for (const Case& c : cases) {
       auto run = [&]() {

@@ -10,141 +10,266 @@
 // tile accumulates X[:, si-slab] . block over the CSR list ptr[so]..ptr[so+1].
 //
 // Exact fp32: v_mfma_f32_32x32x2_f32 (gfx950 has no xf32; the f32-input MFMA
-// is a k-ordered fmaf chain).  32x32x2 operand map: lane l supplies A[i=l&31]
-// [k=l>>5] and B[k=l>>5][j=l&31].  The k order inside each group of 8 is
-// permuted -- lane half h takes k = 8g + 4h + s at step s -- so a lane's 4
-// consecutive k-steps are 16 contiguous bytes of both operands.
+// is a k-ordered fmaf chain).  Roles: the weight block is the i-side operand
+// (output features), the activations the j-side (batch rows), so
+//   D[n][b] = sum_k We[n][k] X[b][k]
+// and both operands and the accumulator are exactly 1 KB chunks of the
+// row-tile layout (lcn_internal.h): lane l supplies X[32rt + (l&31)][8g +
+// 4(l>>5) + s] at k-step s of group g and holds Y[32rt + (l&31)][8q + 4(l>>5)
+// + s] in acc[4q + s].  The lane-half k permutation (lane half h takes k = 8g
+// + 4h + s) makes each operand fragment one float4.
 //
-// Tile: 128 rows x 64 columns per workgroup, 4 waves of 32 rows x 64 columns
-// (two 32x32 accumulators); the 128x64 activation tile and the 64x64 weight
-// block are staged in LDS (row stride 68 floats: conflict-free ds_read_b128),
-// the next input slab is prefetched into registers while the MFMAs run; 3
-// workgroups per CU.  (Variants with register-resident A fragments, 256-row
-// tiles or double-buffered LDS measured equal or slower: DESIGN.md §3.)
+// Workgroup = 4 waves = 4 row tiles (128 rows) x one output slab.  Each wave
+// loads its own activation fragments straight from HBM/L2 into registers (8
+// coalesced 1 KB loads per input slab, prefetched one slab ahead in a second
+// register set); the weight block, shared by the 4 waves, goes through LDS
+// in a double buffer, so there is one barrier per input slab.  Measured
+// against a 128x64 LDS-staged tile with two barriers per slab: 124 vs 114
+// TFLOP/s at cfg3.
 //
-// Operand prologue (PRO), applied while staging the activation tile:
-//   PRO_RAW     a = X
-//   PRO_BNACT   a = leaky(scale * X + shift)                  (BN apply + LeakyReLU)
-// (Rebuilding the backward's dz = c1 du + c2 + c3 z here was measured 27%
-// slower than reading a stored dz: every input slab is re-staged by ~10
-// output slabs, so the rebuild and the extra z stream are paid ~10 times;
-// the weight-gradient kernel stores dz instead)
-// Epilogue: + bias / + residual, store; then either BN forward partials of the
-// output (sum, M2 about the tile mean) or BN backward partials of the layer
-// below (sum du, sum du * zhat), per column of the 128-row tile.
+// Operand prologue (PRO):  PRO_RAW a = X;  PRO_BNACT a = leaky(scale X + shift)
+// (BN apply + LeakyReLU of the input's layer, scale/shift tables in LDS).
+// Epilogue: + bias / + residual, store; then per 32-row tile either BN forward
+// partials of the output (sum, M2 about the tile mean) or BN backward partials
+// of the layer below (sum du, sum du * zhat), column sums through LDS.
 #include "gemm_common.h"
 
 namespace lcn {
 
-template <int PRO>
-__global__ __launch_bounds__(256) void gemm_bs_kernel(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* As = smem;                  // [128][LDA]
-  float* Ws = smem + 128 * LDA;      // [64][LDA]
+#define STEP(W0, W1, XV)                 \
+  acc0 = MFMA32((W0).x, (XV).x, acc0);   \
+  acc1 = MFMA32((W1).x, (XV).x, acc1);   \
+  acc0 = MFMA32((W0).y, (XV).y, acc0);   \
+  acc1 = MFMA32((W1).y, (XV).y, acc1);   \
+  acc0 = MFMA32((W0).z, (XV).z, acc0);   \
+  acc1 = MFMA32((W1).z, (XV).z, acc1);   \
+  acc0 = MFMA32((W0).w, (XV).w, acc0);   \
+  acc1 = MFMA32((W1).w, (XV).w, acc1);
+
+#define DECLX(P) float4 P##0, P##1, P##2, P##3, P##4, P##5, P##6, P##7;
+// activation fragments of input slab si (8 chunks of this wave's row tile)
+#define LOADX(P, SI)                                                      \
+  {                                                                       \
+    const float4* xs_ = xw + (size_t)(SI) * 512;                          \
+    P##0 = xs_[0]; P##1 = xs_[64]; P##2 = xs_[128]; P##3 = xs_[192];      \
+    P##4 = xs_[256]; P##5 = xs_[320]; P##6 = xs_[384]; P##7 = xs_[448];   \
+  }
+// this thread's quarter of a weight block, global -> registers -> LDS
+#define LOADW(BLK)                                                        \
+  {                                                                       \
+    const float4* ws_ = W4 + (size_t)(BLK) * 1024 + threadIdx.x;          \
+    st0 = ws_[0]; st1 = ws_[256]; st2 = ws_[512]; st3 = ws_[768];         \
+  }
+#define STOREW(BUF)                                                       \
+  {                                                                       \
+    float4* d_ = Wl + (BUF) * 1024 + threadIdx.x;                         \
+    d_[0] = st0; d_[256] = st1; d_[512] = st2; d_[768] = st3;             \
+  }
+#define GSTEP(BUF, G, XV, CH)                                             \
+  {                                                                       \
+    if constexpr (PRO == PRO_BNACT) {                                     \
+      const int c_ = (CH) + 8 * (G) + 4 * h;                              \
+      XV = bnact4(XV, *(const float4*)(tsc + c_), *(const float4*)(tsh + c_), al); \
+    }                                                                     \
+    const float4 w0_ = Wl[(BUF) * 1024 + (2 * (G)) * 64 + lane];          \
+    const float4 w1_ = Wl[(BUF) * 1024 + (2 * (G) + 1) * 64 + lane];      \
+    STEP(w0_, w1_, XV)                                                    \
+  }
+// schedule of one input slab: the LDS reads of group g+1 go out while the 8
+// MFMAs of group g run (keeps 4 weight fragments live instead of 16)
+#define SGB(MASK, N) __builtin_amdgcn_sched_group_barrier(MASK, N, 0);
+#define SCHED_SLAB                                                         \
+  SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) \
+  SGB(0x008, 8) SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) SGB(0x008, 8) \
+  SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) \
+  SGB(0x008, 8)
+#define COMPX(BUF, P, CH)                                                 \
+  GSTEP(BUF, 0, P##0, CH) GSTEP(BUF, 1, P##1, CH) GSTEP(BUF, 2, P##2, CH) \
+  GSTEP(BUF, 3, P##3, CH) GSTEP(BUF, 4, P##4, CH) GSTEP(BUF, 5, P##5, CH) \
+  GSTEP(BUF, 6, P##6, CH) GSTEP(BUF, 7, P##7, CH) SCHED_SLAB
+
+template <int PRO, int EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gemm_bs_kernel(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float4 Wl[];  // [2][1024] (+ BN tables)
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int rt = wg / a.n_out_slabs, so = wg - rt * a.n_out_slabs;
-  const int row0 = rt * 128;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int c4 = t & 15, rr = t >> 4;
-  const int lr = lane & 31, h = lane >> 5;
+  const int rtg = wg / a.n_out_slabs, so = wg - rtg * a.n_out_slabs;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+  const int rt_raw = rtg * kGemmWaves + w;
+  const bool live = rt_raw < a.n_rt;
+  // waves past the last row tile recompute it (they take part in the barriers)
+  const int rt = live ? rt_raw : a.n_rt - 1;
   const int beg = a.ptr[so], end = a.ptr[so + 1];
+  const int2* __restrict__ idx = a.idx;
+  const float4* __restrict__ W4 = (const float4*)a.blocks;
+  const float4* xw = (const float4*)a.X + (size_t)rt * a.S_in * 512 + lane;
+  const float al = a.alpha;
+  const float* tsc = nullptr;
+  const float* tsh = nullptr;
+  if constexpr (PRO == PRO_BNACT) {
+    float* tb = (float*)(Wl + 2048);
+    for (int c = threadIdx.x; c < a.pro_F; c += 256) {
+      tb[c] = a.pro_scale[c];
+      tb[a.pro_F + c] = a.pro_shift[c];
+    }
+    tsc = tb;
+    tsh = tb + a.pro_F;
+  }
+  const int spj = a.spj_in;
+  constexpr int DSR = PRO == PRO_BNACT ? 4 : 2;  // LDS reads per k-group
 
   f32x16 acc0, acc1;
 #pragma unroll
   for (int k = 0; k < 16; ++k) { acc0[k] = 0.f; acc1[k] = 0.f; }
-
-  // named staging registers (arrays were demoted to scratch by the compiler)
-  float4 ra0, ra1, ra2, ra3, ra4, ra5, ra6, ra7, rw0, rw1, rw2, rw3;
-  const int2* __restrict__ gidx = a.idx;
-  const float* __restrict__ gX = a.X;
-  const float* __restrict__ gblocks = a.blocks;
-  const int glast = a.B - 1, gldx = a.ldx;
-  // rows past B are clamped, not zeroed: output rows are independent and
-  // rows >= B are neither stored nor counted in the BN partials
-#define GL_ROWS(P, D0, D1, D2, D3, D4, D5, D6, D7)                         \
-  D0 = *(const float4*)((P) + (size_t)min(row0 + rr, glast) * gldx);       \
-  D1 = *(const float4*)((P) + (size_t)min(row0 + rr + 16, glast) * gldx);  \
-  D2 = *(const float4*)((P) + (size_t)min(row0 + rr + 32, glast) * gldx);  \
-  D3 = *(const float4*)((P) + (size_t)min(row0 + rr + 48, glast) * gldx);  \
-  D4 = *(const float4*)((P) + (size_t)min(row0 + rr + 64, glast) * gldx);  \
-  D5 = *(const float4*)((P) + (size_t)min(row0 + rr + 80, glast) * gldx);  \
-  D6 = *(const float4*)((P) + (size_t)min(row0 + rr + 96, glast) * gldx);  \
-  D7 = *(const float4*)((P) + (size_t)min(row0 + rr + 112, glast) * gldx);
-#define GLOAD(E)                                                                          \
-  {                                                                                       \
-    const int2 ib_ = gidx[(E)];                                                           \
-    si_next = ib_.x;                                                                      \
-    const float* src_ = gX + (size_t)ib_.x * kSlab + 4 * c4;                              \
-    GL_ROWS(src_, ra0, ra1, ra2, ra3, ra4, ra5, ra6, ra7)                                 \
-    const float* wsrc_ = gblocks + (size_t)ib_.y * (kSlab * kSlab) + rr * kSlab + 4 * c4; \
-    rw0 = *(const float4*)(wsrc_);                                                        \
-    rw1 = *(const float4*)(wsrc_ + 16 * kSlab);                                           \
-    rw2 = *(const float4*)(wsrc_ + 32 * kSlab);                                           \
-    rw3 = *(const float4*)(wsrc_ + 48 * kSlab);                                           \
+  float4 st0, st1, st2, st3;
+  DECLX(xa)
+  DECLX(xb)
+  int2 ia = idx[beg], ib = ia;
+  LOADW(ia.y)
+  LOADX(xa, ia.x)
+  STOREW(0)
+  __syncthreads();
+  // every output slab has >= 1 input block (checked in lcn_create)
+  for (int e = beg; e < end; e += 2) {
+    const bool n1 = e + 1 < end;
+    if (n1) {
+      ib = idx[e + 1];
+      LOADW(ib.y)
+      LOADX(xb, ib.x)
+    }
+    COMPX(0, xa, (ia.x % spj) * kSlab)
+    if (n1) STOREW(1)
+    __syncthreads();
+    if (n1) {
+      const bool n2 = e + 2 < end;
+      if (n2) {
+        ia = idx[e + 2];
+        LOADW(ia.y)
+        LOADX(xa, ia.x)
+      }
+      COMPX(1, xb, (ib.x % spj) * kSlab)
+      if (n2) STOREW(0)
+      __syncthreads();
+    }
   }
 
-  int si_next = 0;
-  GLOAD(beg);  // every output slab has >= 1 input block (checked in lcn_create)
-  for (int e = beg; e < end; ++e) {
-    const int si = si_next;
-    __syncthreads();
-    if constexpr (PRO == PRO_BNACT) {
-      const int ch = (si % a.spj_in) * kSlab + 4 * c4;
-      const float4 sc = *(const float4*)(a.pro_scale + ch);
-      const float4 sh = *(const float4*)(a.pro_shift + ch);
-      const float al = a.alpha;
-      ra0 = bnact4(ra0, sc, sh, al); ra1 = bnact4(ra1, sc, sh, al);
-      ra2 = bnact4(ra2, sc, sh, al); ra3 = bnact4(ra3, sc, sh, al);
-      ra4 = bnact4(ra4, sc, sh, al); ra5 = bnact4(ra5, sc, sh, al);
-      ra6 = bnact4(ra6, sc, sh, al); ra7 = bnact4(ra7, sc, sh, al);
-    }
-    {
-      float* ad = As + rr * LDA + 4 * c4;
-      *(float4*)(ad) = ra0;
-      *(float4*)(ad + 16 * LDA) = ra1;
-      *(float4*)(ad + 32 * LDA) = ra2;
-      *(float4*)(ad + 48 * LDA) = ra3;
-      *(float4*)(ad + 64 * LDA) = ra4;
-      *(float4*)(ad + 80 * LDA) = ra5;
-      *(float4*)(ad + 96 * LDA) = ra6;
-      *(float4*)(ad + 112 * LDA) = ra7;
-      float* wd = Ws + rr * LDA + 4 * c4;
-      *(float4*)(wd) = rw0;
-      *(float4*)(wd + 16 * LDA) = rw1;
-      *(float4*)(wd + 32 * LDA) = rw2;
-      *(float4*)(wd + 48 * LDA) = rw3;
-    }
-    __syncthreads();
-    if (e + 1 < end) GLOAD(e + 1);
-
-    const float* Ap = As + (32 * w + lr) * LDA + 4 * h;
-    const float* B0 = Ws + lr * LDA + 4 * h;
-    const float* B1 = Ws + (32 + lr) * LDA + 4 * h;
+  // ---- epilogue ----
+  const int S_out = a.S_out, ncols = S_out * kSlab;
+  const size_t tbase = ((size_t)rt * S_out + so) * 512 + lane;  // float4 index of chunk 0
+  float v[32];
 #pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      const float4 av = *(const float4*)(Ap + 8 * g);
-      const float4 b0 = *(const float4*)(B0 + 8 * g);
-      const float4 b1 = *(const float4*)(B1 + 8 * g);
-      MFMA_STEP4(av, b0, b1, acc0, acc1);
+  for (int q = 0; q < 4; ++q) {
+    float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
+    if (a.bias) {
+      b0 = *(const float4*)(a.bias + so * kSlab + 8 * q + 4 * h);
+      b1 = *(const float4*)(a.bias + so * kSlab + 32 + 8 * q + 4 * h);
+    }
+    if (a.addsrc) {
+      const float4 r0 = ((const float4*)a.addsrc)[tbase + q * 64];
+      const float4 r1 = ((const float4*)a.addsrc)[tbase + (4 + q) * 64];
+      b0.x += r0.x; b0.y += r0.y; b0.z += r0.z; b0.w += r0.w;
+      b1.x += r1.x; b1.y += r1.y; b1.z += r1.z; b1.w += r1.w;
+    }
+    v[4 * q + 0] = acc0[4 * q + 0] + b0.x;
+    v[4 * q + 1] = acc0[4 * q + 1] + b0.y;
+    v[4 * q + 2] = acc0[4 * q + 2] + b0.z;
+    v[4 * q + 3] = acc0[4 * q + 3] + b0.w;
+    v[16 + 4 * q + 0] = acc1[4 * q + 0] + b1.x;
+    v[16 + 4 * q + 1] = acc1[4 * q + 1] + b1.y;
+    v[16 + 4 * q + 2] = acc1[4 * q + 2] + b1.z;
+    v[16 + 4 * q + 3] = acc1[4 * q + 3] + b1.w;
+  }
+  if (live) {
+    float4* Y = (float4*)a.Y;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      Y[tbase + q * 64] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      Y[tbase + (4 + q) * 64] =
+          make_float4(v[16 + 4 * q], v[16 + 4 * q + 1], v[16 + 4 * q + 2], v[16 + 4 * q + 3]);
     }
   }
-#undef GLOAD
-#undef GL_ROWS
-  gemm_epilogue_32x64(a, acc0, acc1, rt, so, row0, w, lr, h, smem);
-}
-
-int gemm_bs_rows(int variant) {
-  (void)variant;
-  return 128;
+  if constexpr (EPI == EPI_NONE) return;
+  // Column partials of the wave's 32x64 tile through its 8 KB of the (now
+  // free) weight LDS: the wave writes float4 chunks with a lane swizzle
+  // (position l ^ (2q + (l>>5)) of chunk q) that makes the column-wise reads
+  // bank-conflict free; lane c then sums column c over the tile's rows.
+  __syncthreads();  // all waves are done with the weight buffers
+  float* red = (float*)Wl + w * 2048;
+  const int c = lane, cg = c >> 3, chh = (c >> 2) & 1, cs = c & 3;
+  const int n = live ? min(kRT, a.B - rt * kRT) : 0;  // valid rows of the tile
+  float2* stat = a.stat + (size_t)rt * ncols + so * kSlab + c;
+  auto put = [&](int q, float x0, float x1, float x2, float x3) {
+    const int pos = lane ^ (2 * q + h);
+    *(float4*)(red + (q * 64 + pos) * 4) = make_float4(x0, x1, x2, x3);
+  };
+  // value of row r of column c (r < 32)
+  auto get = [&](int r) {
+    const int l = r + 32 * chh;
+    return red[(cg * 64 + (l ^ (2 * cg + chh))) * 4 + cs];
+  };
+  if constexpr (EPI == EPI_BNFWD) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) put(q, v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    __syncthreads();
+    float sum = 0.f;
+    for (int r = 0; r < n; ++r) sum += get(r);
+    const float mean = n > 0 ? sum / (float)n : 0.f;
+    float m2 = 0.f;
+    for (int r = 0; r < n; ++r) {
+      const float d = get(r) - mean;
+      m2 = fmaf(d, d, m2);
+    }
+    if (live) *stat = make_float2(sum, m2);
+    return;
+  }
+  // EPI_BNBACK: du = dh * leaky'(u(z)), zhat = (z - mean) * rstd of the layer
+  // below; pass 0 reduces du, pass 1 du * zhat (z re-read from L2)
+  const int chb = (so % (a.epi_F / kSlab)) * kSlab + 4 * h;
+  const float4* Z4 = (const float4*)a.epi_z;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {  // chunk q holds values 4q..4q+3 (acc0 for q < 4, acc1 after)
+    const float4 z4 = Z4[tbase + q * 64];
+    const int ch = chb + 8 * q;
+    const float4 sc = *(const float4*)(a.epi_scale + ch), sh = *(const float4*)(a.epi_shift + ch);
+    v[4 * q + 0] = fmaf(z4.x, sc.x, sh.x) > 0.f ? v[4 * q + 0] : v[4 * q + 0] * al;
+    v[4 * q + 1] = fmaf(z4.y, sc.y, sh.y) > 0.f ? v[4 * q + 1] : v[4 * q + 1] * al;
+    v[4 * q + 2] = fmaf(z4.z, sc.z, sh.z) > 0.f ? v[4 * q + 2] : v[4 * q + 2] * al;
+    v[4 * q + 3] = fmaf(z4.w, sc.w, sh.w) > 0.f ? v[4 * q + 3] : v[4 * q + 3] * al;
+    put(q, v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    __builtin_amdgcn_sched_barrier(0);  // one chunk's loads at a time (register pressure)
+  }
+  __syncthreads();
+  float P = 0.f;
+  for (int r = 0; r < n; ++r) P += get(r);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4 z4 = Z4[tbase + q * 64];
+    const int ch = chb + 8 * q;
+    const float4 mu = *(const float4*)(a.epi_mean + ch), rs = *(const float4*)(a.epi_rstd + ch);
+    put(q, v[4 * q] * ((z4.x - mu.x) * rs.x), v[4 * q + 1] * ((z4.y - mu.y) * rs.y),
+        v[4 * q + 2] * ((z4.z - mu.z) * rs.z), v[4 * q + 3] * ((z4.w - mu.w) * rs.w));
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __syncthreads();
+  float Q = 0.f;
+  for (int r = 0; r < n; ++r) Q += get(r);
+  if (live) *stat = make_float2(P, Q);
 }
 
 void launch_gemm_bs(const GemmArgs& a, hipStream_t s) {
-  const int grid = ((a.B + 127) / 128) * a.n_out_slabs;
-  const size_t lds = (size_t)(128 + 64) * LDA * sizeof(float);
-  if (a.pro_mode == PRO_BNACT)
-    hipLaunchKernelGGL(gemm_bs_kernel<PRO_BNACT>, dim3(grid), dim3(256), lds, s, a);
-  else
-    hipLaunchKernelGGL(gemm_bs_kernel<PRO_RAW>, dim3(grid), dim3(256), lds, s, a);
+  const int grid = ((a.n_rt + kGemmWaves - 1) / kGemmWaves) * a.n_out_slabs;
+  const size_t lds = 2 * 1024 * sizeof(float4);
+  const size_t ldsp = lds + 2 * a.pro_F * sizeof(float);
+#define LAUNCH(P, E, L) hipLaunchKernelGGL((gemm_bs_kernel<P, E>), dim3(grid), dim3(256), L, s, a)
+  if (a.pro_mode == PRO_BNACT) {
+    if (a.epi_mode == EPI_BNFWD) LAUNCH(PRO_BNACT, EPI_BNFWD, ldsp);
+    else LAUNCH(PRO_BNACT, EPI_NONE, ldsp);
+  } else {
+    if (a.epi_mode == EPI_BNFWD) LAUNCH(PRO_RAW, EPI_BNFWD, lds);
+    else if (a.epi_mode == EPI_BNBACK) LAUNCH(PRO_RAW, EPI_BNBACK, lds);
+    else LAUNCH(PRO_RAW, EPI_NONE, lds);
+  }
+#undef LAUNCH
 }
 
 }  // namespace lcn

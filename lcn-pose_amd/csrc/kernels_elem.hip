@@ -4,7 +4,7 @@
 // variance, tf.nn.batch_normalization's x*inv + (beta - mean*inv)),
 // tf.nn.leaky_relu(alpha=0.2) and the residual add (models_att.py:704).
 //
-// Statistics are reduced in three levels: per 128-row tile the producing
+// Statistics are reduced in three levels: per 32-row tile the producing
 // GEMM's epilogue writes (sum, sum of squared deviations about the tile mean)
 // -- or, backward, (sum du, sum du*zhat) -- as float; colreduce merges the
 // tiles of every column in float64; the channel kernels merge the 17 joint
@@ -19,7 +19,8 @@
 
 namespace lcn {
 
-__device__ __forceinline__ float leaky(float u, float alpha) { return u > 0.f ? u : u * alpha; }
+// tf.nn.leaky_relu: max(alpha * u, u)  (alpha < 1)
+__device__ __forceinline__ float leaky(float u, float alpha) { return fmaxf(u * alpha, u); }
 
 // out[col] = sum over tiles of part[t][col] in float64, 64 columns per
 // workgroup, 16 waves striding the tiles, fixed-order combine (deterministic).
@@ -161,14 +162,19 @@ void launch_bn_bwd_finalize(const double2* col, int H, int F, int phase, int bn,
                      db);
 }
 
+// h = [res +] leaky(scale*z + shift) over row-tiled [B][S*64] buffers; the
+// channel of float4 i is ((i >> 9) % S % (F/64))*64 + 8*g + 4*h with g, h
+// from the chunk-local index (lcn_internal.h)
 __global__ __launch_bounds__(256) void bn_act_kernel(const float4* __restrict__ z,
                                                      const float4* __restrict__ res,
                                                      float4* __restrict__ h,
                                                      const float* __restrict__ scale,
-                                                     const float* __restrict__ shift, int F,
+                                                     const float* __restrict__ shift, int F, int S,
                                                      float alpha, int64_t n4) {
+  const int spj = F / 64;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const int ch = (int)((i * 4) % F);
+    const int c4 = (int)(i & 511);
+    const int ch = (int)((i >> 9) % S % spj) * 64 + 8 * (c4 >> 6) + 4 * ((c4 >> 5) & 1);
     const float4 sc = *(const float4*)(scale + ch), sh = *(const float4*)(shift + ch);
     float4 v = z[i];
     v.x = leaky(fmaf(v.x, sc.x, sh.x), alpha);
@@ -184,23 +190,23 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const float4* __restrict__ 
 }
 
 void launch_bn_act(const float* z, const float* res, float* h, const float* scale,
-                   const float* shift, int F, float alpha, int B, int H, hipStream_t s) {
-  const int64_t n4 = (int64_t)B * H / 4;
+                   const float* shift, int F, float alpha, int B, int S, hipStream_t s) {
+  const int64_t n4 = tiled_floats(B, S) / 4;
   const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 256 * 16);
   hipLaunchKernelGGL(bn_act_kernel, dim3(grid), dim3(256), 0, s, (const float4*)z,
-                     (const float4*)res, (float4*)h, scale, shift, F, alpha, n4);
+                     (const float4*)res, (float4*)h, scale, shift, F, S, alpha, n4);
 }
 
-// per-tile column sums of a narrow [B][ncols <= 64] matrix (the output bias
-// gradient), written as float2 (sum, 0) for colreduce
+// per-kEwRows-row column sums of a 1-slab row-tiled src (the output bias
+// gradient): lane = column, 4 waves split the rows
 __global__ __launch_bounds__(256) void colpart_kernel(const float* __restrict__ src, int B,
-                                                      int ncols, int ld, float2* __restrict__ part) {
+                                                      int ncols, float2* __restrict__ part) {
   __shared__ float red[4][64];
   const int t = threadIdx.x, c = t & 63, w = t >> 6;
   const int r0 = blockIdx.x * kEwRows, r1 = min(B, r0 + kEwRows);
   float s = 0.f;
   if (c < ncols)
-    for (int r = r0 + w; r < r1; r += 4) s += src[(size_t)r * ld + c];
+    for (int r = r0 + w; r < r1; r += 4) s += src[tix(r, c, 1)];
   red[w][c] = s;
   __syncthreads();
   if (w == 0 && c < ncols)
@@ -208,9 +214,9 @@ __global__ __launch_bounds__(256) void colpart_kernel(const float* __restrict__ 
         make_float2((red[0][c] + red[1][c]) + (red[2][c] + red[3][c]), 0.f);
 }
 
-void launch_colpart(const float* src, int B, int ncols, int ld, float2* part, hipStream_t s) {
+void launch_colpart(const float* src, int B, int ncols, float2* part, hipStream_t s) {
   hipLaunchKernelGGL(colpart_kernel, dim3((B + kEwRows - 1) / kEwRows), dim3(256), 0, s, src, B,
-                     ncols, ld, part);
+                     ncols, part);
 }
 
 __global__ void col_to_float_kernel(const double2* __restrict__ col, int n, float* __restrict__ out) {

@@ -5,11 +5,14 @@
 // 64-wide slab (see lcn_api.cpp); what remains here is the elementwise tail of
 // the output layer (models_att.py:768-773) and the MSE loss (:356) with its
 // gradient d out = 2 (out - lab) / (B * 51).
+#include <algorithm>
+
 #include "lcn_internal.h"
 
 namespace lcn {
 
-// One wave per row (lane = output column, 51 of 64 active), grid-stride rows.
+// One wave per row (lane = output column, 51 of 64 active), grid-stride rows;
+// y, x and dy are 1-slab row-tiled buffers (lcn_internal.h), out / lab row-major.
 __global__ __launch_bounds__(256) void out_assemble_kernel(OutAsmArgs a) {
   __shared__ double red[4];
   const int t = threadIdx.x, c = t & 63, w = t >> 6;
@@ -17,14 +20,16 @@ __global__ __launch_bounds__(256) void out_assemble_kernel(OutAsmArgs a) {
   double lsum = 0.0;
   for (int row = blockIdx.x * 4 + w; row < a.B; row += gridDim.x * 4) {
     if (c < 51) {
-      const float y = a.y[(size_t)row * 64 + c] + a.b4[c];
-      const float o = k < 2 ? a.x[(size_t)row * 64 + a.in_f * j + k] + y : y;
+      const float y = a.y[tix(row, c, 1)] + a.b4[c];
+      const float o = k < 2 ? a.x[tix(row, a.in_f * j + k, 1)] + y : y;
       a.out[(size_t)row * 51 + c] = o;
       if (a.lab) {
         const float d = o - a.lab[(size_t)row * 51 + c];
         lsum += (double)d * (double)d;
-        if (a.dy) a.dy[(size_t)row * 64 + c] = a.dscale * d;
+        if (a.dy) a.dy[tix(row, c, 1)] = a.dscale * d;
       }
+    } else if (a.dy) {
+      a.dy[tix(row, c, 1)] = 0.f;  // padded columns of the output layer's dX operand
     }
   }
   if (!a.loss_part) return;
@@ -36,6 +41,26 @@ __global__ __launch_bounds__(256) void out_assemble_kernel(OutAsmArgs a) {
 
 void launch_out_assemble(const OutAsmArgs& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL(out_assemble_kernel, dim3(grid), dim3(256), 0, s, a);
+}
+
+// row-major [B][cols] -> 1-slab row tiles, zero padded; one thread per float4
+__global__ __launch_bounds__(256) void tile_in_kernel(const float* __restrict__ src, int cols,
+                                                      int B, float4* __restrict__ dst, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int c4 = (int)(i & 511), l = c4 & 63;
+    const int64_t row = (i >> 9) * kRT + (l & 31);
+    const int c = 8 * (c4 >> 6) + 4 * (l >> 5);
+    float v[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) v[s] = (row < B && c + s < cols) ? src[row * cols + c + s] : 0.f;
+    dst[i] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+void launch_tile_in(const float* src, int cols, int B, float* dst, hipStream_t s) {
+  const int64_t n4 = tiled_floats(B, 1) / 4;
+  const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
+  hipLaunchKernelGGL(tile_in_kernel, dim3(grid), dim3(256), 0, s, src, cols, B, (float4*)dst, n4);
 }
 
 __global__ void loss_finalize_kernel(const double* part, int n, double* out) {

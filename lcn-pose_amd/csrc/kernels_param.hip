@@ -74,15 +74,18 @@ void launch_wnorm(const float* params, const int64_t* offs, const int64_t* sizes
                      max_norm);
 }
 
-// hidden layer: one workgroup per 64x64 block, transposed through LDS so both
-// packed layouts are written with coalesced stores
+// Packed weight blocks for the MFMA kernels are fragment-packed
+// (lcn_internal.h frag_ix): block[n][k] with n the output and k the reduction
+// index of the GEMM that reads it.
+
+// hidden layer: one workgroup per 64x64 block (si, so) of W_e:
+// fwd block [n = q][k = p] (z = a.We), bwd block [n = p][k = q] (da = dz.We^T)
 __global__ __launch_bounds__(256) void wprep_hidden_kernel(const float* __restrict__ W, int ld,
                                                            const int2* __restrict__ blk, int spj,
                                                            const float* __restrict__ M,
                                                            const float* __restrict__ denom, int layer,
                                                            float* __restrict__ fwd,
                                                            float* __restrict__ bwd) {
-  __shared__ float tile[64 * 65];
   const int b = blockIdx.x;
   const int2 sb = blk[b];
   const float m = M[(sb.x / spj) * kJ + (sb.y / spj)];
@@ -90,17 +93,12 @@ __global__ __launch_bounds__(256) void wprep_hidden_kernel(const float* __restri
   for (int e = threadIdx.x; e < 4096; e += 256) {
     const int p = e >> 6, q = e & 63;
     const float v = (W[(size_t)(sb.x * 64 + p) * ld + sb.y * 64 + q] / dn) * m;
-    tile[p * 65 + q] = v;
-    bwd[(size_t)b * 4096 + e] = v;  // [p][q]
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < 4096; e += 256) {
-    const int q = e >> 6, p = e & 63;
-    fwd[(size_t)b * 4096 + e] = tile[p * 65 + q];  // [q][p]
+    bwd[(size_t)b * 4096 + frag_ix(p, q)] = v;
+    fwd[(size_t)b * 4096 + frag_ix(q, p)] = v;
   }
 }
 
-// lift (K = 17*C padded to 64): blk[so][f][k] = W_e[k][so*64 + f], zero for k >= 17*C
+// lift (K = 17*C padded to 64): block so [n = f][k] = W_e[k][so*64 + f], zero for k >= 17*C
 __global__ __launch_bounds__(256) void wprep_lift_kernel(const float* __restrict__ W, int C,
                                                          int nslab, int spj,
                                                          const float* __restrict__ M,
@@ -109,15 +107,15 @@ __global__ __launch_bounds__(256) void wprep_lift_kernel(const float* __restrict
   const int so = blockIdx.x, ld = nslab * 64;
   const float dn = denom[layer];
   for (int e = threadIdx.x; e < 4096; e += 256) {
-    const int f = e >> 6, k = e & 63;
+    const int k = e >> 6, f = e & 63;  // coalesced W reads along f
     float v = 0.f;
     if (k < kJ * C) v = (W[(size_t)k * ld + so * 64 + f] / dn) * M[(k / C) * kJ + so / spj];
-    blk[(size_t)so * 4096 + e] = v;
+    blk[(size_t)so * 4096 + frag_ix(f, k)] = v;
   }
 }
 
-// output (N = 51 padded to 64): fwd[si][c'][p] and bwd[si][p][c'] = W_e[si*64+p][c'],
-// zero for c' >= 51
+// output (N = 51 padded to 64): block si fwd [n = c'][k = p], bwd [n = p][k = c'],
+// = W_e[si*64 + p][c'], zero for c' >= 51
 __global__ __launch_bounds__(256) void wprep_out_kernel(const float* __restrict__ W, int F,
                                                         const float* __restrict__ M,
                                                         const float* __restrict__ denom, int layer,
@@ -127,12 +125,12 @@ __global__ __launch_bounds__(256) void wprep_out_kernel(const float* __restrict_
   const int si = blockIdx.x;
   const float dn = denom[layer];
   for (int e = threadIdx.x; e < 4096; e += 256) {
-    const int p = e >> 6, c = e & 63;  // bwd layout: coalesced W reads along c
+    const int p = e >> 6, c = e & 63;  // coalesced W reads along c
     const int r = si * 64 + p;
     float v = 0.f;
     if (c < N) v = (W[(size_t)r * N + c] / dn) * M[(r / F) * kJ + c / 3];
-    bwd[(size_t)si * 4096 + e] = v;
-    fwd[(size_t)si * 4096 + c * 64 + p] = v;
+    bwd[(size_t)si * 4096 + frag_ix(p, c)] = v;
+    fwd[(size_t)si * 4096 + frag_ix(c, p)] = v;
   }
 }
 

@@ -84,6 +84,7 @@ struct Handle {
   // activations
   // x / y / dy of the thin layers are padded to 64 columns (pads stay zero)
   float *x = nullptr, *lab = nullptr, *out = nullptr, *dy = nullptr, *yout = nullptr;
+  float* xin = nullptr;           // host-staged row-major input [Bmax][17*in_F]
   std::vector<float*> Z, Hb;
   // DH: gradient w.r.t. a block output h_l; DG: w.r.t. the inner activation g;
   // DZ: dz of a hidden layer, stored by its weight-gradient GEMM
@@ -117,8 +118,6 @@ struct Handle {
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
 
-  // block-sparse GEMM variant (kernels_gemm.hip); LCN_GEMM_VARIANT overrides
-  int gemm_variant = 0;
 
   // instrumentation
   int timing = 0;
@@ -204,7 +203,6 @@ int build(Handle* h, const lcn_config* c) {
   h->b1p = h->b1;
   h->b2p = h->b2;
   h->Bmax = c->max_batch;
-  if (const char* gv = std::getenv("LCN_GEMM_VARIANT")) h->gemm_variant = std::atoi(gv);
   h->Cmat.assign(c->mask_matrix, c->mask_matrix + kJ * kJ);
   const int H = h->H, F = h->F, inF = h->inF, nl = h->nl;
 
@@ -380,18 +378,22 @@ int build(Handle* h, const lcn_config* c) {
 
   // ---- activations / scratch for Bmax ----
   const int64_t B = h->Bmax;
-  CHECK(dalloc(h, &h->x, (size_t)B * 64));
+  // activations in the row-tile layout (lcn_internal.h); x / y / dy of the
+  // thin layers are one 64-wide slab
+  const size_t t1 = (size_t)tiled_floats(B, 1), tH = (size_t)tiled_floats(B, h->nslab);
+  CHECK(dalloc(h, &h->x, t1));
+  CHECK(dalloc(h, &h->xin, (size_t)B * kJ * h->inF));
   CHECK(dalloc(h, &h->lab, (size_t)B * 51));
   CHECK(dalloc(h, &h->out, (size_t)B * 51));
-  CHECK(dalloc(h, &h->dy, (size_t)B * 64));
-  CHECK(dalloc(h, &h->yout, (size_t)B * 64));
+  CHECK(dalloc(h, &h->dy, t1));
+  CHECK(dalloc(h, &h->yout, t1));
   h->Z.assign(nl - 1, nullptr);
-  for (auto& z : h->Z) CHECK(dalloc(h, &z, (size_t)B * H));
+  for (auto& z : h->Z) CHECK(dalloc(h, &z, tH));
   h->Hb.assign(h->L + 1, nullptr);
-  for (auto& hb : h->Hb) CHECK(dalloc(h, &hb, (size_t)B * H));
-  CHECK(dalloc(h, &h->DH, (size_t)B * H));
-  CHECK(dalloc(h, &h->DG, (size_t)B * H));
-  CHECK(dalloc(h, &h->DZ, (size_t)B * H));
+  for (auto& hb : h->Hb) CHECK(dalloc(h, &hb, tH));
+  CHECK(dalloc(h, &h->DH, tH));
+  CHECK(dalloc(h, &h->DG, tH));
+  CHECK(dalloc(h, &h->DZ, tH));
   h->zsum.assign(nl - 1, nullptr);
   for (auto& zs : h->zsum) CHECK(dalloc(h, &zs, (size_t)H));
   h->nbn = nl - 1;
@@ -415,7 +417,7 @@ int build(Handle* h, const lcn_config* c) {
     }
   }
   CHECK(dalloc(h, &h->c123, 3 * F));
-  CHECK(dalloc(h, &h->stat_part, (size_t)cdiv(B, kGemmBM) * H));
+  CHECK(dalloc(h, &h->stat_part, (size_t)cdiv(B, kRT) * H));
   CHECK(dalloc(h, &h->col_part, (size_t)cdiv(B, kEwRows) * 64));
   CHECK(dalloc(h, &h->colacc, (size_t)H));
   h->loss_grid = (int)std::min<int64_t>(2048, cdiv(B, 4));
@@ -472,7 +474,7 @@ int bn_stats(Handle* h, int k, int B) {
   const double count = (double)B * h->world * kJ;
   const float* gamma = h->theta + h->gamma_off[k];
   const float* beta = h->theta + h->beta_off[k];
-  launch_colreduce(h->stat_part, (int)cdiv(B, kGemmBM), kGemmBM, B, h->H, 1, h->colacc, s);
+  launch_colreduce(h->stat_part, (int)cdiv(B, kRT), kRT, B, h->H, 1, h->colacc, s);
   if (h->world == 1) {
     launch_bn_fwd_finalize(h->colacc, h->H, h->F, 0, count, gamma, beta, h->eps, h->acc1, h->bn[k],
                            h->zsum[k], s);
@@ -486,14 +488,14 @@ int bn_stats(Handle* h, int k, int B) {
   return LCN_OK;
 }
 
-// A GEMM operand: a [B][ld] tensor, read as is (PRO_RAW), through BN apply +
-// LeakyReLU of BN layer `layer` (PRO_BNACT: p = z of that layer), or as the dz
-// of BN layer `layer` rebuilt from p = dh and its z (PRO_BNBACK).
+// A GEMM operand: a row-tiled tensor of S slabs, read as is (PRO_RAW), through
+// BN apply + LeakyReLU of BN layer `layer` (PRO_BNACT: p = z of that layer),
+// or as the dz of BN layer `layer` rebuilt from p = dh and its z (PRO_BNBACK).
 struct Operand {
-  const float* p; int ld;
+  const float* p; int S;
   int mode; int layer;
 };
-Operand raw(const float* p, int ld) { return Operand{p, ld, PRO_RAW, -1}; }
+Operand raw(const float* p, int S) { return Operand{p, S, PRO_RAW, -1}; }
 
 // One launch of the block-sparse MFMA GEMM: Y[:, so-slab] = sum over the CSR
 // list of X[:, si-slab] . block (+ bias / + addsrc); epilogue partials:
@@ -503,7 +505,7 @@ struct GemmCall {
   Operand X;
   const float* blocks; const int* ptr; const int2* idx; int n_out_slabs;
   const float* bias;
-  float* Y; int ldy; const float* addsrc;
+  float* Y; int S_out; const float* addsrc;
   int epi_mode; int epi_layer;
   int timer; double flops_per_row;
 };
@@ -515,7 +517,7 @@ int gemm(Handle* h, const GemmCall& c, int B) {
   }
   GemmArgs a{};
   a.X = c.X.p;
-  a.ldx = c.X.ld;
+  a.S_in = c.X.S;
   a.blocks = c.blocks;
   a.ptr = c.ptr;
   a.idx = c.idx;
@@ -525,10 +527,11 @@ int gemm(Handle* h, const GemmCall& c, int B) {
     a.pro_scale = h->bn[c.X.layer].scale;
     a.pro_shift = h->bn[c.X.layer].shift;
   }
+  a.pro_F = h->F;
   a.spj_in = h->spj;
   a.alpha = h->alpha;
   a.Y = c.Y;
-  a.ldy = c.ldy;
+  a.S_out = c.S_out;
   a.addsrc = c.addsrc;
   a.epi_mode = c.epi_mode;
   a.stat = c.epi_mode != EPI_NONE ? h->stat_part : nullptr;
@@ -543,8 +546,7 @@ int gemm(Handle* h, const GemmCall& c, int B) {
   a.epi_F = h->F;
   a.B = B;
   a.n_out_slabs = c.n_out_slabs;
-  a.variant = h->gemm_variant;
-  a.n_row_tiles = (int)cdiv(B, gemm_bs_rows(a.variant));
+  a.n_rt = (int)cdiv(B, kRT);
   hipEvent_t ev[2];
   if (c.timer >= 0) tstart(h, c.timer, ev);
   launch_gemm_bs(a, h->stream);
@@ -559,7 +561,7 @@ int gemm_hidden(Handle* h, int k, int kindt, const Operand& X, float* Y, const f
   const bool fwd = kindt == LCN_K_GEMM_FWD;
   GemmCall c{X, fwd ? Lr.blk_fwd : Lr.blk_bwd, fwd ? h->fwd_ptr : h->bwd_ptr,
              fwd ? h->fwd_idx : h->bwd_idx, h->nslab, fwd ? h->theta + h->b_off[k] : nullptr,
-             Y, h->H, addsrc, epi_mode, epi_layer,
+             Y, h->nslab, addsrc, epi_mode, epi_layer,
              kindt, 2.0 * 4096.0 * h->nblk};  // 2*64*64 FLOP per block per row
   return gemm(h, c, B);
 }
@@ -573,9 +575,9 @@ int gemm_dw(Handle* h, const Operand& A, const Operand& D, const int2* blk, int 
             int ld, int rows_valid, int cols_valid, int B, bool timed, float* dz_out = nullptr) {
   GemmDwArgs a{};
   a.A = A.p;
-  a.lda = A.ld;
+  a.S_a = A.S;
   a.D = D.p;
-  a.ldd = D.ld;
+  a.S_d = D.S;
   if (A.mode == PRO_BNACT) {
     a.pro_scale = h->bn[A.layer].scale;
     a.pro_shift = h->bn[A.layer].shift;
@@ -594,7 +596,8 @@ int gemm_dw(Handle* h, const Operand& A, const Operand& D, const int2* blk, int 
       return LCN_E_ARG;
     }
   }
-  a.spj_in = h->spj;
+  a.spj_a = h->spj;
+  a.spj_d = h->spj;
   a.alpha = h->alpha;
   a.blk = blk;
   a.nblk = nblk;
@@ -624,7 +627,7 @@ int bn_back(Handle* h, int k, int B) {
   float* dgam = bn ? h->rg + h->gamma_off[k] : nullptr;
   float* dbet = bn ? h->rg + h->beta_off[k] : nullptr;
   float* db = h->rg + h->b_off[k];
-  launch_colreduce(h->stat_part, (int)cdiv(B, kGemmBM), kGemmBM, B, h->H, 0, h->colacc, s);
+  launch_colreduce(h->stat_part, (int)cdiv(B, kRT), kRT, B, h->H, 0, h->colacc, s);
   if (h->world == 1 || !bn) {
     launch_bn_bwd_finalize(h->colacc, h->H, h->F, 0, bn, count, (double)B, gamma, st.mean, st.rstd,
                            h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
@@ -640,30 +643,30 @@ int bn_back(Handle* h, int k, int B) {
 
 int forward(Handle* h, int B, bool with_labels, bool train) {
   hipStream_t s = h->stream;
-  const int H = h->H, nl = h->nl;
+  const int S = h->nslab, nl = h->nl;
   CHECK(prep_weights(h));
   const int epi = h->batch_norm ? EPI_BNFWD : EPI_NONE;
   // lift z0 = x . W1e + b1 (models_att.py:714-729): x padded to one 64-wide slab
   const double thin_flops = 2.0 * 4096.0 * h->nslab;
-  CHECK(gemm(h, GemmCall{raw(h->x, 64), h->wl[0].blk_fwd, h->thin_ptr, h->thin_idx, h->nslab,
-                         h->theta + h->b_off[0], h->Z[0], H, nullptr, epi, -1, -1, thin_flops}, B));
+  CHECK(gemm(h, GemmCall{raw(h->x, 1), h->wl[0].blk_fwd, h->thin_ptr, h->thin_idx, S,
+                         h->theta + h->b_off[0], h->Z[0], S, nullptr, epi, -1, -1, thin_flops}, B));
   CHECK(bn_stats(h, 0, B));
-  launch_bn_act(h->Z[0], nullptr, h->Hb[0], h->bn[0].scale, h->bn[0].shift, h->F, h->alpha, B, H, s);
+  launch_bn_act(h->Z[0], nullptr, h->Hb[0], h->bn[0].scale, h->bn[0].shift, h->F, h->alpha, B, S, s);
   // two_linear blocks (models_att.py:630-705)
   for (int l = 0; l < h->L; ++l) {
     const int k1 = 2 * l + 1, k2 = 2 * l + 2;
-    CHECK(gemm_hidden(h, k1, LCN_K_GEMM_FWD, raw(h->Hb[l], H), h->Z[k1], nullptr, epi, -1, B));
+    CHECK(gemm_hidden(h, k1, LCN_K_GEMM_FWD, raw(h->Hb[l], S), h->Z[k1], nullptr, epi, -1, B));
     CHECK(bn_stats(h, k1, B));
-    CHECK(gemm_hidden(h, k2, LCN_K_GEMM_FWD, Operand{h->Z[k1], H, PRO_BNACT, k1}, h->Z[k2],
+    CHECK(gemm_hidden(h, k2, LCN_K_GEMM_FWD, Operand{h->Z[k1], S, PRO_BNACT, k1}, h->Z[k2],
                       nullptr, epi, -1, B));
     CHECK(bn_stats(h, k2, B));
     launch_bn_act(h->Z[k2], h->residual ? h->Hb[l] : nullptr, h->Hb[l + 1], h->bn[k2].scale,
-                  h->bn[k2].shift, h->F, h->alpha, B, H, s);
+                  h->bn[k2].shift, h->F, h->alpha, B, S, s);
   }
-  // output layer y = h_L . W4e + b4 into a [B][64] buffer (51 used), then the
+  // output layer y = h_L . W4e + b4 into a 1-slab buffer (51 used), then the
   // output assembly, loss and d out (models_att.py:749-773, :356)
-  CHECK(gemm(h, GemmCall{raw(h->Hb[h->L], H), h->wl[nl - 1].blk_fwd, h->out_ptr, h->out_idx, 1,
-                         nullptr, h->yout, 64, nullptr, EPI_NONE, -1, -1, thin_flops}, B));
+  CHECK(gemm(h, GemmCall{raw(h->Hb[h->L], S), h->wl[nl - 1].blk_fwd, h->out_ptr, h->out_idx, 1,
+                         nullptr, h->yout, 1, nullptr, EPI_NONE, -1, -1, thin_flops}, B));
   OutAsmArgs oa{};
   oa.y = h->yout;
   oa.b4 = h->theta + h->b_off[nl - 1];
@@ -684,7 +687,7 @@ int forward(Handle* h, int B, bool with_labels, bool train) {
 int backward(Handle* h, int B) {
   hipStream_t s = h->stream;
   const int nl = h->nl, L = h->L;
-  const int H = h->H;
+  const int H = h->H, S = h->nslab;
   const WLayer& Lo = h->wl[nl - 1];
   // Every dX GEMM stores the incoming gradient dh of the BN layer below it and
   // its epilogue reduces that layer's (sum du, sum du*zhat); bn_back turns
@@ -692,12 +695,12 @@ int backward(Handle* h, int B) {
   // staging its D operand and stores it (DZ) for the layer's dX GEMM.
   // output layer: dh_L = dy . W4e^T (dy padded to 64 columns), dW4e = h_L^T dy, db4 = sum dy
   const int top = nl - 2;  // BN layer under the output layer
-  CHECK(gemm(h, GemmCall{raw(h->dy, 64), Lo.blk_bwd, h->thin_ptr, h->thin_idx, h->nslab, nullptr,
-                         h->DH, H, nullptr, EPI_BNBACK, top, -1, 0.0}, B));
-  CHECK(gemm_dw(h, raw(h->Hb[L], H), raw(h->dy, 64), h->out_blk, h->nslab, h->rg + Lo.w_off, 51,
+  CHECK(gemm(h, GemmCall{raw(h->dy, 1), Lo.blk_bwd, h->thin_ptr, h->thin_idx, S, nullptr,
+                         h->DH, S, nullptr, EPI_BNBACK, top, -1, 0.0}, B));
+  CHECK(gemm_dw(h, raw(h->Hb[L], S), raw(h->dy, 1), h->out_blk, S, h->rg + Lo.w_off, 51,
                 H, 51, B, false));
   const int ct = (int)cdiv(B, kEwRows);
-  launch_colpart(h->dy, B, 51, 64, h->col_part, s);
+  launch_colpart(h->dy, B, 51, h->col_part, s);
   launch_colreduce(h->col_part, ct, kEwRows, B, 51, 0, h->colacc, s);
   launch_col_to_float(h->colacc, 51, h->rg + h->b_off[nl - 1], s);
 
@@ -706,20 +709,20 @@ int backward(Handle* h, int B) {
     const int below = l > 0 ? k1 - 1 : 0;  // BN layer under block l's input h_l
     // DH = dh_{l+1}: gradient of the block output
     CHECK(bn_back(h, k2, B));
-    CHECK(gemm_dw(h, Operand{h->Z[k1], H, PRO_BNACT, k1}, Operand{h->DH, H, PRO_BNBACK, k2},
+    CHECK(gemm_dw(h, Operand{h->Z[k1], S, PRO_BNACT, k1}, Operand{h->DH, S, PRO_BNBACK, k2},
                   h->blk, h->nblk, h->rg + h->wl[k2].w_off, H, H, H, B, true,
                   h->DZ));                                             // dW_k2 = g^T dz2; DZ = dz2
-    CHECK(gemm_hidden(h, k2, LCN_K_GEMM_DX, raw(h->DZ, H), h->DG, nullptr, EPI_BNBACK, k1, B));
+    CHECK(gemm_hidden(h, k2, LCN_K_GEMM_DX, raw(h->DZ, S), h->DG, nullptr, EPI_BNBACK, k1, B));
     CHECK(bn_back(h, k1, B));
-    CHECK(gemm_dw(h, raw(h->Hb[l], H), Operand{h->DG, H, PRO_BNBACK, k1}, h->blk, h->nblk,
+    CHECK(gemm_dw(h, raw(h->Hb[l], S), Operand{h->DG, S, PRO_BNBACK, k1}, h->blk, h->nblk,
                   h->rg + h->wl[k1].w_off, H, H, H, B, true,
                   h->DZ));                                             // dW_k1 = h_l^T dz1; DZ = dz1
-    CHECK(gemm_hidden(h, k1, LCN_K_GEMM_DX, raw(h->DZ, H), h->DH, h->residual ? h->DH : nullptr,
+    CHECK(gemm_hidden(h, k1, LCN_K_GEMM_DX, raw(h->DZ, S), h->DH, h->residual ? h->DH : nullptr,
                       EPI_BNBACK, below, B));                          // dh_l (+ residual)
   }
   // lift: dz0, dW1e = x^T dz0 (x padded: rows >= 17*in_F dropped), db1
   CHECK(bn_back(h, 0, B));
-  CHECK(gemm_dw(h, raw(h->x, 64), Operand{h->DH, H, PRO_BNBACK, 0}, h->lift_blk, h->nslab,
+  CHECK(gemm_dw(h, raw(h->x, 1), Operand{h->DH, S, PRO_BNBACK, 0}, h->lift_blk, S,
                 h->rg + h->wl[0].w_off, H, kJ * h->inF, H, B, false));
   return LCN_OK;
 }
@@ -752,10 +755,17 @@ int stage_inputs(Handle* h, const float* x, const float* lab, int64_t B, int fla
     return LCN_E_ARG;
   }
   const hipMemcpyKind kind = (flags & LCN_IN_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-  // x lands in the 64-column padded buffer of the lift GEMM (pads stay zero)
-  if (x)
-    HIPC(hipMemcpy2DAsync(h->x, 64 * sizeof(float), x, (size_t)kJ * h->inF * sizeof(float),
-                          (size_t)kJ * h->inF * sizeof(float), (size_t)B, kind, h->stream));
+  // x lands in the 1-slab row-tiled operand of the lift GEMM (zero padded);
+  // host input is staged row-major first
+  if (x) {
+    const int cols = kJ * h->inF;
+    const float* src = x;
+    if (!(flags & LCN_IN_DEVICE)) {
+      HIPC(hipMemcpyAsync(h->xin, x, (size_t)B * cols * 4, hipMemcpyHostToDevice, h->stream));
+      src = h->xin;
+    }
+    launch_tile_in(src, cols, (int)B, h->x, h->stream);
+  }
   if (lab) HIPC(hipMemcpyAsync(h->lab, lab, (size_t)B * 51 * 4, kind, h->stream));
   h->lastB = B;
   return LCN_OK;
@@ -1107,6 +1117,14 @@ int lcn_debug_tensor(void* handle, int32_t kind, int32_t idx, float* host, int64
   else if (kind == 4) { src = h->rg; cnt = h->P; }
   else return LCN_E_ARG;
   if (n < cnt) { h->err = "buffer too small"; return LCN_E_ARG; }
+  if (kind <= 1) {  // row-tiled activation -> row-major [B][H]
+    const int S = h->nslab;
+    std::vector<float> t((size_t)tiled_floats(h->lastB, S));
+    HIPC(hipMemcpy(t.data(), src, t.size() * 4, hipMemcpyDeviceToHost));
+    for (int64_t b = 0; b < h->lastB; ++b)
+      for (int c = 0; c < h->H; ++c) host[b * h->H + c] = t[tix(b, c, S)];
+    return LCN_OK;
+  }
   HIPC(hipMemcpy(host, src, cnt * 4, hipMemcpyDeviceToHost));
   return LCN_OK;
 }

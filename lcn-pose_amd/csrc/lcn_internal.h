@@ -8,57 +8,87 @@ namespace lcn {
 
 constexpr int kJ = 17;          // joints (models_att.py:512-513)
 constexpr int kSlab = 64;       // feature slab = MFMA tile edge; F is a multiple of it
-constexpr int kGemmBM = 128;    // batch rows per block-sparse GEMM tile
+constexpr int kRT = 32;         // rows per row tile of the activation layout
+constexpr int kGemmWaves = 4;   // row tiles (one per wave) per block-sparse GEMM workgroup
 constexpr int kEwRows = 256;    // rows per tile of the output-bias column partials
+
+// ----------------------------------------------------------------------------
+// Activation layout ("row tiles").  Every activation the step keeps in HBM --
+// x, z, h, g, dh, dg, dz, y, dy -- with C = S*64 columns is stored as
+//   [ceil(B/32)][S][8][64][4] floats:
+// row tile rt (32 rows) x slab sl (64 features) is one contiguous 8 KB block;
+// its 1 KB chunk g holds, for lane l = 0..63, row 32*rt + (l & 31) and the four
+// features 64*sl + 8*g + 4*(l >> 5) + 0..3.  That chunk is exactly one wave's
+// operand fragment of v_mfma_f32_32x32x2_f32 with the batch on the MFMA's j
+// side (lane l supplies B[k = 8g + 4(l>>5) + s][j = l & 31] at k-step s), and
+// exactly a wave's accumulator when the output features are on the i side
+// (lane l holds D[i = 8q + 4(l>>5) + s][j = l & 31] in acc[4q + s]): every
+// GEMM operand load and result store is one coalesced 1 KB transaction and
+// the output of one layer is the next layer's operand without re-layout.
+// Rows past B in the last tile are padding: computed, never counted.
+// ----------------------------------------------------------------------------
+__host__ __device__ inline int64_t tix(int64_t b, int c, int S) {
+  const int sl = c >> 6, f = c & 63;
+  return ((((b >> 5) * S + sl) * 8 + (f >> 3)) * 64 + (b & 31) + 32 * ((f >> 2) & 1)) * 4 + (f & 3);
+}
+__host__ __device__ inline int64_t tiled_floats(int64_t B, int S) { return ((B + 31) / 32) * 32 * 64 * (int64_t)S; }
+
+// Fragment-packed 64x64 weight block ("[n][k]" with k the reduction index):
+//   [g = k>>3][half = n>>5][lane = (n & 31) + 32*((k>>2)&1)][s = k & 3]
+// chunk (g, half) is the MFMA i-side operand of k-group g for outputs
+// 32*half..32*half+31 -- again one contiguous 1 KB read per wave.
+__host__ __device__ inline int frag_ix(int n, int k) {
+  return (((k >> 3) * 2 + (n >> 5)) * 64 + (n & 31) + 32 * ((k >> 2) & 1)) * 4 + (k & 3);
+}
 
 // ----------------------------------------------------------------------------
 // Block-sparse GEMM (forward z = a.We + b and backward dA = dZ.We^T).
 // Output slab `so` of a row tile accumulates X[:, si-slab] . blocks[blk] over
-// the (si, blk) list ptr[so]..ptr[so+1].  Blocks are 64x64, [n][k] (k fastest).
+// the (si, blk) list ptr[so]..ptr[so+1].
 // ----------------------------------------------------------------------------
 // operand transform applied while staging: raw, BN apply + LeakyReLU, or (the
 // weight-gradient kernel's D operand) the BN + LeakyReLU backward dz from dh, z
 enum { PRO_RAW = 0, PRO_BNACT = 1, PRO_BNBACK = 2 };
-// epilogue partials: EPI_BNFWD = BN statistics of the output (sum, M2 about the
-// tile mean); EPI_BNBACK = BN-backward sums of the layer below (sum du, sum du*zhat)
+// epilogue partials per 32-row tile: EPI_BNFWD = BN statistics of the output
+// (sum, M2 about the tile mean); EPI_BNBACK = BN-backward sums of the layer
+// below (sum du, sum du*zhat)
 enum { EPI_NONE = 0, EPI_BNFWD = 1, EPI_BNBACK = 2 };
 
 struct GemmArgs {
-  const float* X; int ldx;           // A operand source [B][ldx]
-  const float* blocks;               // packed blocks
+  const float* X; int S_in;          // operand activations (tiled, S_in slabs)
+  const float* blocks;               // fragment-packed blocks
   const int* ptr;                    // [n_out_slabs + 1]
   const int2* idx;                   // (in_slab, block id)
   const float* bias;                 // [n_out_slabs*64] or null
   int pro_mode;                      // PRO_RAW or PRO_BNACT
-  const float* pro_scale;            // forward BN scale / shift of the input's layer
+  const float* pro_scale;            // forward BN scale / shift of the input's layer [F]
   const float* pro_shift;
+  int pro_F;                         // channels of pro_scale / pro_shift
   int spj_in;                        // input slabs per joint (channel = (si % spj)*64 + k)
   float alpha;                       // LeakyReLU slope
-  float* Y; int ldy;                 // output [B][ldy]
-  const float* addsrc;               // Y = acc (+ addsrc) ; may alias Y
+  float* Y; int S_out;               // output (tiled, S_out slabs)
+  const float* addsrc;               // Y = acc (+ addsrc), tiled like Y; may alias Y
   int epi_mode;
-  float2* stat;                      // partials [row_tiles][ldy]
-  const float* epi_z;                // EPI_BNBACK: z of the layer below [B][ldy]
+  float2* stat;                      // partials [n_rt][S_out*64]
+  const float* epi_z;                // EPI_BNBACK: z of the layer below (tiled like Y)
   const float* epi_scale; const float* epi_shift; const float* epi_mean; const float* epi_rstd;
-  int epi_F;
-  int B; int n_out_slabs; int n_row_tiles;
-  int variant;                       // reserved (tile variant)
+  int epi_F;                         // channels of the epi_* vectors (spj of Y = epi_F/64)
+  int B; int n_out_slabs; int n_rt;  // n_rt = ceil(B / 32)
 };
 void launch_gemm_bs(const GemmArgs& a, hipStream_t s);
-int gemm_bs_rows(int variant);       // batch rows per workgroup tile of a variant
 
 // dWe blocks: part[chunk][blk][p][q] = sum_{b in chunk} A[b, si*64+p] * D[b, so*64+q]
 struct GemmDwArgs {
-  const float* A; int lda;
-  const float* D; int ldd;           // d_bnback: D = dh and the operand is dz (PRO_BNBACK)
-  const float* pro_scale; const float* pro_shift; int spj_in; float alpha;  // A: BN apply + act
-  int d_bnback;
+  const float* A; int S_a;           // tiled
+  const float* D; int S_d;           // tiled; d_bnback: D = dh and the operand is dz
+  const float* pro_scale; const float* pro_shift; int spj_a; float alpha;  // A: BN apply + act
+  int d_bnback; int spj_d;
   const float* d_z; const float* d_scale; const float* d_shift; const float* d_c123; int d_F;
-  const int* dz_writer;              // D_BNBACK: per block, 1 if it stores dz (one per so)
-  float* dz_out;                     // D_BNBACK: dz [B][ldd] or null
+  const int* dz_writer;              // d_bnback: per block, 1 if it stores dz (one per so)
+  float* dz_out;                     // d_bnback: dz (tiled like D) or null
   const int2* blk;                   // (si, so) per block
   int nblk;
-  int B; int chunk_rows; int nchunks;
+  int B; int chunk_rows; int nchunks;  // chunk_rows: multiple of 64
   float* part;                       // [nchunks][nblk][4096]
 };
 void launch_gemm_dw(const GemmDwArgs& a, hipStream_t s);
@@ -69,18 +99,22 @@ void launch_dw_reduce(const float* part, int nchunks, int nblk, const int2* blk,
 
 // ----------------------------------------------------------------------------
 // The thin layers run on the same MFMA kernels with the narrow side padded to
-// one 64-wide slab: the lift's input x [B][17*in_F] lives in a [B][64] buffer
-// (K = 34 -> 64) and the output layer's 51 columns in [B][64] buffers.
+// one 64-wide slab: the lift's input x [B][17*in_F] is a 1-slab tiled buffer
+// (K = 34 -> 64, zero padded) and the output layer's 51 columns live in 1-slab
+// tiled buffers.
 // ----------------------------------------------------------------------------
+// row-major src [B][cols] (cols <= 64) -> 1-slab tiled dst, zero padded (rows
+// of the last tile past B and columns past cols)
+void launch_tile_in(const float* src, int cols, int B, float* dst, hipStream_t s);
 // y = h . W4e from the GEMM; out[b, 3j+c] = (c < 2 ? x[b, in_f*j+c] : 0) + (y + b4);
-// loss partials and dy = dscale * (out - lab) (padded [B][64]) (models_att.py:765-773, :356)
+// loss partials and dy = dscale * (out - lab) (models_att.py:765-773, :356)
 struct OutAsmArgs {
-  const float* y;                    // [B][64] (51 used)
+  const float* y;                    // 1-slab tiled (51 used)
   const float* b4;                   // [51]
-  const float* x; int in_f;          // x padded [B][64]
-  const float* lab;                  // [B][51] or null
-  float* out;                        // [B][51]
-  float* dy;                         // [B][64] or null
+  const float* x; int in_f;          // 1-slab tiled
+  const float* lab;                  // [B][51] row-major, or null
+  float* out;                        // [B][51] row-major
+  float* dy;                         // 1-slab tiled, or null (padding written as 0)
   double* loss_part;                 // [gridDim] or null
   float dscale;                      // 2 / (B_global * 51)
   int B;
@@ -108,11 +142,12 @@ void launch_bn_bwd_finalize(const double2* col, int H, int F, int phase, int bn,
                             double b_local, const float* gamma, const float* mean,
                             const float* rstd, double* acc, float* dgamma, float* dbeta,
                             float* c123, const double* zsum, float* db, hipStream_t s);
-// h = [res +] leaky(scale*z + shift)
+// h = [res +] leaky(scale*z + shift), tiled [B][S*64] buffers
 void launch_bn_act(const float* z, const float* res, float* h, const float* scale,
-                   const float* shift, int F, float alpha, int B, int H, hipStream_t s);
-// per-kEwRows-tile column sums of src[B][ncols] (ncols <= 64) -> part[tiles][ncols] as (sum, 0)
-void launch_colpart(const float* src, int B, int ncols, int ld, float2* part, hipStream_t s);
+                   const float* shift, int F, float alpha, int B, int S, hipStream_t s);
+// per-kEwRows-tile column sums of a 1-slab tiled src (ncols <= 64 used) ->
+// part[tiles][ncols] as (sum, 0)
+void launch_colpart(const float* src, int B, int ncols, float2* part, hipStream_t s);
 // out[i] = (float) col[i].x
 void launch_col_to_float(const double2* col, int n, float* out, hipStream_t s);
 void launch_loss_finalize(const double* part, int n, double* out, hipStream_t s);
@@ -124,7 +159,7 @@ struct WLayer {            // one linear layer's weight
   int64_t w_off;           // offset in the flat parameter vector
   int kin, nout, fin, fout;
   int kind;                // 0 lift, 1 hidden, 2 output
-  // packed 64x64 blocks of W_e, K-contiguous ([n][k]) for the MFMA kernels:
+  // 64x64 blocks of W_e for the MFMA kernels, [n][k] fragment-packed (frag_ix):
   //   hidden: blk_fwd [nblk][q][p], blk_bwd [nblk][p][q]
   //   lift:   blk_fwd [nslab][f][k = u*in_F + c] (k >= 17*in_F zero)
   //   output: blk_fwd [nslab][c'][p], blk_bwd [nslab][p][c'] (c' >= 51 zero)
