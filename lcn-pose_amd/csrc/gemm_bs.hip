@@ -75,14 +75,15 @@ namespace lcn {
     const float4 w1_ = Wl[(BUF) * 1024 + (2 * (G) + 1) * 64 + lane];      \
     STEP(w0_, w1_, XV)                                                    \
   }
-// schedule of one input slab: the LDS reads of group g+1 go out while the 8
-// MFMAs of group g run (keeps 4 weight fragments live instead of 16)
+// schedule of one input slab: the LDS reads of group g+1 are issued before
+// the 8 MFMAs of group g, so their latency hides under those MFMAs
 #define SGB(MASK, N) __builtin_amdgcn_sched_group_barrier(MASK, N, 0);
-#define SCHED_SLAB                                                         \
-  SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) \
-  SGB(0x008, 8) SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) SGB(0x008, 8) \
-  SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) \
-  SGB(0x008, 8)
+#define SCHED_SLAB                                                          \
+  SGB(0x100, DSR)                                                           \
+  SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) SGB(0x008, 8)               \
+  SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) SGB(0x008, 8)               \
+  SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) SGB(0x008, 8)               \
+  SGB(0x100, DSR) SGB(0x008, 8) SGB(0x008, 8)
 #define COMPX(BUF, P, CH)                                                 \
   GSTEP(BUF, 0, P##0, CH) GSTEP(BUF, 1, P##1, CH) GSTEP(BUF, 2, P##2, CH) \
   GSTEP(BUF, 3, P##3, CH) GSTEP(BUF, 4, P##4, CH) GSTEP(BUF, 5, P##5, CH) \

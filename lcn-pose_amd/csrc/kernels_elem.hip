@@ -22,85 +22,102 @@ namespace lcn {
 // tf.nn.leaky_relu: max(alpha * u, u)  (alpha < 1)
 __device__ __forceinline__ float leaky(float u, float alpha) { return fmaxf(u * alpha, u); }
 
-// out[col] = sum over tiles of part[t][col] in float64, 64 columns per
-// workgroup, 16 waves striding the tiles, fixed-order combine (deterministic).
-//   mode 0: (sum x, sum y)          mode 1: (sum x, sum (y + x^2 / n_t))
-__global__ __launch_bounds__(1024) void colreduce_kernel(const float2* __restrict__ part,
-                                                         int n_tiles, int tile_rows, int B, int H,
-                                                         int mode, double2* __restrict__ out) {
-  __shared__ double2 red[16][64];
+// Column sums of tile partials part[n_tiles][H] in float64, split over
+// kColSplit tile groups (grid.y) so the reduction fills the chip:
+// out[p][col] = sum over tiles t of group p (t = 4p + w mod 4P, waves w) of
+//   mode 0: (x, y)          mode 1: (x, y + x^2 / n_t)
+// fixed-order combines throughout (deterministic).  The finish kernels add
+// the kColSplit groups.
+__global__ __launch_bounds__(256) void colreduce_kernel(const float2* __restrict__ part,
+                                                        int n_tiles, int tile_rows, int B, int H,
+                                                        int mode, double2* __restrict__ out) {
+  __shared__ double2 red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + lane;
+  const int col = blockIdx.x * 64 + lane, p = blockIdx.y, P = gridDim.y;
   double a = 0.0, b = 0.0;
   if (col < H) {
-#pragma unroll 4
-    for (int t = w; t < n_tiles; t += 16) {
-      const float2 p = part[(size_t)t * H + col];
-      a += (double)p.x;
+    for (int t = 4 * p + w; t < n_tiles; t += 4 * P) {
+      const float2 v = part[(size_t)t * H + col];
+      a += (double)v.x;
       if (mode == 1) {
         const double nt = (double)min(tile_rows, B - t * tile_rows);
-        b += (double)p.y + (double)p.x * (double)p.x / nt;
+        b += (double)v.y + (double)v.x * (double)v.x / nt;
       } else {
-        b += (double)p.y;
+        b += (double)v.y;
       }
     }
   }
   red[w][lane] = make_double2(a, b);
   __syncthreads();
-  if (w == 0 && col < H) {
-    double sa = 0.0, sb = 0.0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) { sa += red[i][lane].x; sb += red[i][lane].y; }
-    out[col] = make_double2(sa, sb);
-  }
+  if (w == 0 && col < H)
+    out[(size_t)p * H + col] = make_double2((red[0][lane].x + red[1][lane].x) + (red[2][lane].x + red[3][lane].x),
+                                            (red[0][lane].y + red[1][lane].y) + (red[2][lane].y + red[3][lane].y));
 }
 
 void launch_colreduce(const float2* part, int n_tiles, int tile_rows, int B, int H, int mode,
                       double2* out, hipStream_t s) {
-  hipLaunchKernelGGL(colreduce_kernel, dim3((H + 63) / 64), dim3(1024), 0, s, part, n_tiles,
-                     tile_rows, B, H, mode, out);
+  hipLaunchKernelGGL(colreduce_kernel, dim3((H + 63) / 64, kColSplit), dim3(256), 0, s, part,
+                     n_tiles, tile_rows, B, H, mode, out);
 }
 
-// Forward BN finish per channel ch (one thread each).  Phase 0: complete;
-// 1: local channel sums -> acc[2F] (and stop); 2: finish from the all-reduced acc.
-// zsum (when given) receives the per-column sums of z (bias-gradient term of
-// the backward).
-__global__ void bn_fwd_finalize_kernel(const double2* __restrict__ col, int H, int F, int phase,
-                                       double count, const float* __restrict__ gamma,
-                                       const float* __restrict__ beta, float eps, double* acc,
-                                       BnStats st, double* __restrict__ zsum) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= F) return;
-  const int J = H / F;
-  double S = 0.0, Q = 0.0;
-  if (phase <= 1) {
-    for (int j = 0; j < J; ++j) {
-      const double2 c = col[j * F + ch];
-      S += c.x;
-      Q += c.y;
-      if (zsum) zsum[j * F + ch] = c.x;
+// Both finish kernels run as ONE workgroup of 1024 threads: first the
+// kColSplit tile groups of every column are added (fixed order) into LDS,
+// then one thread per channel adds its 17 joint columns and finishes.
+__device__ __forceinline__ void colsum_groups_lds(const double2* __restrict__ col, int H,
+                                                  double2* cs) {
+  for (int c = threadIdx.x; c < H; c += blockDim.x) {
+    double x = 0.0, y = 0.0;
+    for (int p = 0; p < kColSplit; ++p) {
+      const double2 v = col[(size_t)p * H + c];
+      x += v.x;
+      y += v.y;
     }
-    if (phase == 1) { acc[ch] = S; acc[F + ch] = Q; return; }
-  } else {
-    S = acc[ch];
-    Q = acc[F + ch];
+    cs[c] = make_double2(x, y);
   }
-  const double mu = S / count;
-  const double var = fmax(0.0, Q / count - mu * mu);
-  const float mean = (float)mu;
-  const float rstd = 1.0f / sqrtf((float)var + eps);  // rsqrt(variance + epsilon)
-  const float inv = rstd * gamma[ch];                  // inv *= scale
-  st.mean[ch] = mean;
-  st.rstd[ch] = rstd;
-  st.scale[ch] = inv;
-  st.shift[ch] = beta[ch] - mean * inv;                // offset - mean * inv
+  __syncthreads();
+}
+
+// Forward BN finish per channel.  Phase 0: complete; 1: local channel sums ->
+// acc[2F] (and stop); 2: finish from the all-reduced acc.  zsum (when given)
+// receives the per-column sums of z (bias-gradient term of the backward).
+__global__ __launch_bounds__(1024) void bn_fwd_finalize_kernel(
+    const double2* __restrict__ col, int H, int F, int phase, double count,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, double* acc,
+    BnStats st, double* __restrict__ zsum) {
+  extern __shared__ double2 cs[];  // [H]
+  if (phase <= 1) colsum_groups_lds(col, H, cs);
+  const int J = H / F;
+  for (int ch = threadIdx.x; ch < F; ch += blockDim.x) {
+    double S = 0.0, Q = 0.0;
+    if (phase <= 1) {
+      for (int j = 0; j < J; ++j) {
+        const double2 c = cs[j * F + ch];
+        S += c.x;
+        Q += c.y;
+        if (zsum) zsum[j * F + ch] = c.x;
+      }
+      if (phase == 1) { acc[ch] = S; acc[F + ch] = Q; continue; }
+    } else {
+      S = acc[ch];
+      Q = acc[F + ch];
+    }
+    const double mu = S / count;
+    const double var = fmax(0.0, Q / count - mu * mu);
+    const float mean = (float)mu;
+    const float rstd = 1.0f / sqrtf((float)var + eps);  // rsqrt(variance + epsilon)
+    const float inv = rstd * gamma[ch];                  // inv *= scale
+    st.mean[ch] = mean;
+    st.rstd[ch] = rstd;
+    st.scale[ch] = inv;
+    st.shift[ch] = beta[ch] - mean * inv;                // offset - mean * inv
+  }
 }
 
 void launch_bn_fwd_finalize(const double2* col, int H, int F, int phase, double count,
                             const float* gamma, const float* beta, float eps, double* acc,
                             BnStats st, double* zsum, hipStream_t s) {
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((F + 255) / 256), dim3(256), 0, s, col, H, F,
-                     phase, count, gamma, beta, eps, acc, st, zsum);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(1), dim3(1024), H * sizeof(double2), s, col, H,
+                     F, phase, count, gamma, beta, eps, acc, st, zsum);
 }
 
 // Backward BN finish per channel:  dz = c1*du + c2 + c3*z,
@@ -111,45 +128,45 @@ void launch_bn_fwd_finalize(const double2* col, int H, int F, int phase, double 
 // dgamma / dbeta / db are the LOCAL contributions (the raw-gradient vector is
 // all-reduced later); c123 uses the global sums.  bn = 0 (no BatchNorm):
 // dz = du and only db is written.  Phases as bn_fwd_finalize.
-__global__ void bn_bwd_finalize_kernel(const double2* __restrict__ col, int H, int F, int phase,
-                                       int bn, double count, double b_local,
-                                       const float* __restrict__ gamma,
-                                       const float* __restrict__ mean,
-                                       const float* __restrict__ rstd, double* acc,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                       float* __restrict__ c123, const double* __restrict__ zsum,
-                                       float* __restrict__ db) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= F) return;
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
+    const double2* __restrict__ col, int H, int F, int phase, int bn, double count,
+    double b_local, const float* __restrict__ gamma, const float* __restrict__ mean,
+    const float* __restrict__ rstd, double* acc, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, float* __restrict__ c123, const double* __restrict__ zsum,
+    float* __restrict__ db) {
+  extern __shared__ double2 cs[];  // [H]
+  colsum_groups_lds(col, H, cs);
   const int J = H / F;
-  if (!bn) {
-    for (int j = 0; j < J; ++j) db[j * F + ch] = (float)col[j * F + ch].x;
-    return;
-  }
-  double S1 = 0.0, S2 = 0.0;
-  if (phase <= 1) {
-    for (int j = 0; j < J; ++j) {
-      const double2 c = col[j * F + ch];
-      S1 += c.x;
-      S2 += c.y;
+  for (int ch = threadIdx.x; ch < F; ch += blockDim.x) {
+    if (!bn) {
+      for (int j = 0; j < J; ++j) db[j * F + ch] = (float)cs[j * F + ch].x;
+      continue;
     }
-    dgamma[ch] = (float)S2;
-    dbeta[ch] = (float)S1;
-    if (phase == 1) { acc[ch] = S1; acc[F + ch] = S2; return; }
-  } else {
-    S1 = acc[ch];
-    S2 = acc[F + ch];
-  }
-  const double rs = rstd[ch];
-  const double c1 = (double)gamma[ch] * rs;
-  const double c3 = -c1 * rs * S2 / count;
-  const double c2 = -c1 * S1 / count - c3 * (double)mean[ch];
-  c123[ch] = (float)c1;
-  c123[F + ch] = (float)c2;
-  c123[2 * F + ch] = (float)c3;
-  for (int j = 0; j < J; ++j) {
-    const int cj = j * F + ch;
-    db[cj] = (float)(c1 * col[cj].x + b_local * c2 + c3 * zsum[cj]);
+    double S1 = 0.0, S2 = 0.0;
+    if (phase <= 1) {
+      for (int j = 0; j < J; ++j) {
+        const double2 c = cs[j * F + ch];
+        S1 += c.x;
+        S2 += c.y;
+      }
+      dgamma[ch] = (float)S2;
+      dbeta[ch] = (float)S1;
+      if (phase == 1) { acc[ch] = S1; acc[F + ch] = S2; continue; }
+    } else {
+      S1 = acc[ch];
+      S2 = acc[F + ch];
+    }
+    const double rs = rstd[ch];
+    const double c1 = (double)gamma[ch] * rs;
+    const double c3 = -c1 * rs * S2 / count;
+    const double c2 = -c1 * S1 / count - c3 * (double)mean[ch];
+    c123[ch] = (float)c1;
+    c123[F + ch] = (float)c2;
+    c123[2 * F + ch] = (float)c3;
+    for (int j = 0; j < J; ++j) {
+      const int cj = j * F + ch;
+      db[cj] = (float)(c1 * cs[cj].x + b_local * c2 + c3 * zsum[cj]);
+    }
   }
 }
 
@@ -157,9 +174,9 @@ void launch_bn_bwd_finalize(const double2* col, int H, int F, int phase, int bn,
                             double b_local, const float* gamma, const float* mean,
                             const float* rstd, double* acc, float* dgamma, float* dbeta,
                             float* c123, const double* zsum, float* db, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((F + 255) / 256), dim3(256), 0, s, col, H, F,
-                     phase, bn, count, b_local, gamma, mean, rstd, acc, dgamma, dbeta, c123, zsum,
-                     db);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(1024), H * sizeof(double2), s, col, H,
+                     F, phase, bn, count, b_local, gamma, mean, rstd, acc, dgamma, dbeta, c123,
+                     zsum, db);
 }
 
 // h = [res +] leaky(scale*z + shift) over row-tiled [B][S*64] buffers; the
@@ -221,7 +238,10 @@ void launch_colpart(const float* src, int B, int ncols, float2* part, hipStream_
 
 __global__ void col_to_float_kernel(const double2* __restrict__ col, int n, float* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = (float)col[i].x;
+  if (i >= n) return;
+  double x = 0.0;
+  for (int p = 0; p < kColSplit; ++p) x += col[(size_t)p * n + i].x;
+  out[i] = (float)x;
 }
 
 void launch_col_to_float(const double2* col, int n, float* out, hipStream_t s) {

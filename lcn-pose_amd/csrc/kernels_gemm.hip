@@ -15,7 +15,7 @@ namespace lcn {
 //
 // Staging: every thread loads 4 float4 of each operand's two 8 KB row-tile
 // slabs (coalesced 1 KB chunks), applies the operand transform, and scatters
-// them transposed into LDS ([feature][row], row stride 72 floats: the scatter
+// them transposed into LDS ([feature][row], row stride 68 floats: the scatter
 // and the ds_read_b128 fragment reads are both bank-conflict free).  The MFMA
 // runs over the batch: lane l supplies A[b][p = l&31] and D[b][q = l&31] for
 // k = b, four consecutive rows per float4 (lane half h takes rows 8g + 4h + s).
@@ -26,7 +26,7 @@ namespace lcn {
 // designated block per output slab also store that dz (dz_out) for the
 // backward-data GEMM that follows, so dz costs one write and no separate
 // elementwise pass.
-constexpr int kDwLd = 72;
+constexpr int kDwLd = 68;
 
 template <bool PRO, bool DBB>
 __global__ __launch_bounds__(256) void gemm_dw_kernel(GemmDwArgs a) {

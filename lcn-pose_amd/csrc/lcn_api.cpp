@@ -96,7 +96,7 @@ struct Handle {
   float* c123 = nullptr;
   float2* stat_part = nullptr;    // [B/128 tiles][H] GEMM epilogue partials
   float2* col_part = nullptr;     // [B/kEwRows tiles][51] output-bias partials
-  double2* colacc = nullptr;      // [H] float64 column sums
+  double2* colacc = nullptr;      // [kColSplit][H] float64 column sums
   float* dw_part = nullptr;
   double *loss_part = nullptr, *loss_sum = nullptr, *acc1 = nullptr, *acc2 = nullptr;
   int loss_grid = 1;
@@ -117,6 +117,9 @@ struct Handle {
   // communication
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
+  // run the multi-GPU (phase 1 -> all-reduce -> phase 2) BN reductions even
+  // with world == 1 (LCN_FORCE_PHASED=1 at create): lets one GPU test that path
+  bool phased = false;
 
 
   // instrumentation
@@ -180,6 +183,7 @@ int dw_chunks(int nblk) { return std::max(1, std::min(64, 8192 / std::max(1, nbl
 // construction
 // ---------------------------------------------------------------------------
 int build(Handle* h, const lcn_config* c) {
+  if (const char* fp = std::getenv("LCN_FORCE_PHASED")) h->phased = std::atoi(fp) != 0;
   h->inF = c->in_f;
   h->F = c->f;
   h->L = c->num_layers;
@@ -419,7 +423,7 @@ int build(Handle* h, const lcn_config* c) {
   CHECK(dalloc(h, &h->c123, 3 * F));
   CHECK(dalloc(h, &h->stat_part, (size_t)cdiv(B, kRT) * H));
   CHECK(dalloc(h, &h->col_part, (size_t)cdiv(B, kEwRows) * 64));
-  CHECK(dalloc(h, &h->colacc, (size_t)H));
+  CHECK(dalloc(h, &h->colacc, (size_t)kColSplit * H));
   h->loss_grid = (int)std::min<int64_t>(2048, cdiv(B, 4));
   CHECK(dalloc(h, &h->loss_part, (size_t)h->loss_grid));
   CHECK(dalloc(h, &h->loss_sum, 4));
@@ -475,7 +479,7 @@ int bn_stats(Handle* h, int k, int B) {
   const float* gamma = h->theta + h->gamma_off[k];
   const float* beta = h->theta + h->beta_off[k];
   launch_colreduce(h->stat_part, (int)cdiv(B, kRT), kRT, B, h->H, 1, h->colacc, s);
-  if (h->world == 1) {
+  if (!h->phased && h->world == 1) {
     launch_bn_fwd_finalize(h->colacc, h->H, h->F, 0, count, gamma, beta, h->eps, h->acc1, h->bn[k],
                            h->zsum[k], s);
     return LCN_OK;
@@ -628,7 +632,7 @@ int bn_back(Handle* h, int k, int B) {
   float* dbet = bn ? h->rg + h->beta_off[k] : nullptr;
   float* db = h->rg + h->b_off[k];
   launch_colreduce(h->stat_part, (int)cdiv(B, kRT), kRT, B, h->H, 0, h->colacc, s);
-  if (h->world == 1 || !bn) {
+  if ((!h->phased && h->world == 1) || !bn) {
     launch_bn_bwd_finalize(h->colacc, h->H, h->F, 0, bn, count, (double)B, gamma, st.mean, st.rstd,
                            h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
     return LCN_OK;
@@ -796,6 +800,8 @@ int lcn_create(const lcn_config* c, int device, void** handle) {
   if (c->abi_version != LCN_ABI_VERSION) { g_create_error = "abi version mismatch"; return LCN_E_ARG; }
   if (c->joints != kJ) { g_create_error = "joints must be 17 (models_att.py:512-513, params_help.py:12)"; return LCN_E_ARG; }
   if (c->f <= 0 || c->f % kSlab) { g_create_error = "F must be a positive multiple of 64"; return LCN_E_ARG; }
+  // the BN finish kernels keep 17*F float64 pairs in one workgroup's LDS (160 KiB)
+  if (c->f > 512) { g_create_error = "F must be <= 512"; return LCN_E_ARG; }
   if (c->in_f != 2 && c->in_f != 3) { g_create_error = "in_F must be 2 or 3"; return LCN_E_ARG; }
   if (c->num_layers < 0 || c->max_batch <= 0) { g_create_error = "bad num_layers / max_batch"; return LCN_E_ARG; }
   if (c->max_batch > (int64_t)INT32_MAX / (kJ * c->f)) { g_create_error = "max_batch too large"; return LCN_E_ARG; }

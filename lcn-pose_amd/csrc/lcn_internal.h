@@ -126,8 +126,10 @@ void launch_out_assemble(const OutAsmArgs& a, int grid, hipStream_t s);
 // ----------------------------------------------------------------------------
 // stats per channel: mean, rstd, scale = gamma*rstd, shift = beta - mean*scale
 struct BnStats { float* mean; float* rstd; float* scale; float* shift; };
-// float64 column sums of tile partials part[n_tiles][H]:
+// float64 column sums of tile partials part[n_tiles][H] into kColSplit
+// tile-group partials out[kColSplit][H] (added up by the finish kernels):
 //   mode 0 (sum x, sum y); mode 1 (sum x, sum (y + x^2 / rows_of_tile))
+constexpr int kColSplit = 8;
 void launch_colreduce(const float2* part, int n_tiles, int tile_rows, int B, int H, int mode,
                       double2* out, hipStream_t s);
 // forward BN finish from colreduce mode-1 sums.  phase 0 complete (single GPU);
@@ -148,7 +150,7 @@ void launch_bn_act(const float* z, const float* res, float* h, const float* scal
 // per-kEwRows-tile column sums of a 1-slab tiled src (ncols <= 64 used) ->
 // part[tiles][ncols] as (sum, 0)
 void launch_colpart(const float* src, int B, int ncols, float2* part, hipStream_t s);
-// out[i] = (float) col[i].x
+// out[i] = (float) sum over the tile groups of col[.][i].x (col from colreduce with H = n)
 void launch_col_to_float(const double2* col, int n, float* out, hipStream_t s);
 void launch_loss_finalize(const double* part, int n, double* out, hipStream_t s);
 

@@ -416,6 +416,141 @@ def backward(cfg: Config, params, cache, lab: np.ndarray, dtype=np.float32,
 
 
 # ----------------------------------------------------------------------------
+# Data-parallel decomposition (SyncBN), as liblcn runs it with world > 1
+# ----------------------------------------------------------------------------
+
+def _tile_moments(z3: np.ndarray, tile_rows: int = 32):
+    """Per-channel (sum z, sum (M2_t + s_t^2 / n_t)) over the 32-row tiles of a
+    shard -- the float64 quantities bn_fwd_finalize all-reduces
+    (lcn-pose_amd/csrc/kernels_elem.hip colreduce mode 1)."""
+    B, _, F = z3.shape
+    S = np.zeros(F)
+    Q = np.zeros(F)
+    for r0 in range(0, B, tile_rows):
+        t = z3[r0:r0 + tile_rows].astype(np.float64)          # [n, J, F]
+        for j in range(J):
+            col = t[:, j, :]
+            s = col.sum(axis=0)
+            m2 = ((col - s / col.shape[0]) ** 2).sum(axis=0)
+            S += s
+            Q += m2 + s * s / col.shape[0]
+    return S, Q
+
+
+def sharded_grads(cfg: Config, params, x: np.ndarray, lab: np.ndarray, allreduce,
+                  world: int, dtype=np.float64):
+    """One rank's view of a data-parallel step: forward with SyncBN statistics
+    (per-shard tile moments -> all-reduce -> mean / biased variance), backward
+    with all-reduced BN-backward sums, LOCAL raw gradients (dW_e, db, dgamma,
+    dbeta) summed over ranks by one all-reduce, then the mask / clip backward
+    on the global raw gradient.  ``allreduce(a)`` returns the elementwise sum of
+    ``a`` over ranks.  Equals ``backward(forward(full batch))`` -- the identity
+    tests/test_distributed.py checks over gloo.  Follows the same reference
+    lines as forward/backward (models_att.py:588-612, 707-775, :356)."""
+    P = {k: np.asarray(v, dtype) for k, v in params.items()}
+    x = np.asarray(x, dtype)
+    B = x.shape[0]
+    Bg = int(allreduce(np.array([float(B)]))[0])
+    M, S_mask = mask_value(cfg, P, dtype)
+    layers = layer_names(cfg)
+    eff = {wn: effective_weight(cfg, P[wn], M, fin, fout) for (wn, _, _, fin, fout) in layers}
+    recs = []
+
+    def lin(a, li):
+        wn, bname, bnp, fin, fout = layers[li]
+        z = a @ eff[wn][0] + P[bname]
+        st = None
+        if bnp is not None:
+            z3 = z.reshape(B, J, fout)
+            S1, Q = _tile_moments(z3)
+            tot = allreduce(np.concatenate([S1, Q]))
+            N = Bg * J
+            mean = tot[:fout] / N
+            var = np.maximum(tot[fout:] / N - mean * mean, 0.0)
+            rstd = 1.0 / np.sqrt(var + cfg.bn_eps)
+            inv = rstd * P[bnp + "_gamma"]
+            u = (z3 * inv + (P[bnp + "_beta"] - mean * inv)).reshape(B, -1)
+            st = dict(mean=mean, rstd=rstd)
+        else:
+            u = z
+        recs.append(dict(a=a, z=z, u=u, st=st))
+        return _act(cfg, u)
+
+    h = lin(x, 0)
+    li = 1
+    for _ in range(cfg.num_layers):
+        hin = h
+        t = lin(lin(hin, li), li + 1)
+        h = hin + t if cfg.residual else t
+        li += 2
+    wn4, bn4, _, _, _ = layers[-1]
+    y = h @ eff[wn4][0] + P[bn4]
+    x3 = x.reshape(B, J, cfg.in_F)
+    y3 = y.reshape(B, J, 3)
+    out = np.concatenate([x3[:, :, :2] + y3[:, :, :2], y3[:, :, 2:3]], axis=2).reshape(B, -1)
+    dy = (2.0 / (Bg * J * 3)) * (out - np.asarray(lab, dtype))     # global-mean loss
+    raw = {wn4: h.T @ dy, bn4: dy.sum(axis=0)}
+    dh = dy @ eff[wn4][0].T
+
+    def bn_back(dh, k):
+        wn, bname, bnp, fin, fout = layers[k]
+        rec = recs[k]
+        du = dh * np.where(rec["u"] > 0, 1.0, cfg.leaky_alpha)
+        if rec["st"] is None:
+            dz = du
+        else:
+            st = rec["st"]
+            z3 = rec["z"].reshape(B, J, fout)
+            zhat = (z3 - st["mean"]) * st["rstd"]
+            du3 = du.reshape(B, J, fout)
+            loc = np.concatenate([du3.sum(axis=(0, 1)), (du3 * zhat).sum(axis=(0, 1))])
+            tot = allreduce(loc)                                    # c123 from global sums
+            N = Bg * J
+            c1 = P[bnp + "_gamma"] * st["rstd"]
+            c3 = -c1 * st["rstd"] * tot[fout:] / N
+            c2 = -c1 * tot[:fout] / N - c3 * st["mean"]
+            dz = (c1 * du3 + c2 + c3 * z3).reshape(B, -1)
+            raw[bnp + "_beta"] = loc[:fout]                         # local contributions
+            raw[bnp + "_gamma"] = loc[fout:]
+        raw[wn] = rec["a"].T @ dz
+        raw[bname] = dz.sum(axis=0)
+        return dz @ eff[wn][0].T
+
+    li = len(layers) - 2
+    for _ in range(cfg.num_layers):
+        dres = dh
+        dh = bn_back(bn_back(dh, li), li - 1)
+        if cfg.residual:
+            dh = dh + dres
+        li -= 2
+    bn_back(dh, 0)
+
+    names = sorted(raw)
+    flat = allreduce(np.concatenate([raw[n].ravel() for n in names]))
+    g, o = {}, 0
+    for n in names:
+        g[n] = flat[o:o + raw[n].size].reshape(raw[n].shape)
+        o += raw[n].size
+    # mask / clip backward and regularisation on the global raw gradient
+    dM = np.zeros((J, J), dtype)
+    for (wn, bname, _, fin, fout) in layers:
+        We, Wc, n = eff[wn]
+        d4 = g[wn].reshape(J, fin, J, fout)
+        dWc = (d4 * M.reshape(J, 1, J, 1)).reshape(We.shape)
+        dM += (d4 * Wc.reshape(J, fin, J, fout)).sum(axis=(1, 3))
+        W = P[wn]
+        g[wn] = dWc / n - (np.sum(dWc * W) / (n ** 3)) * W if (cfg.max_norm and n > 1) else dWc
+    if cfg.regularization not in (0, None):
+        for (wn, bname, _, _, _) in layers:
+            g[wn] = g[wn] + cfg.regularization * P[wn]
+            g[bname] = g[bname] + cfg.regularization * P[bname]
+    if cfg.learnable_mask:
+        dS = dM * structure(cfg).astype(dtype)
+        g["mask"] = S_mask * (dS - (S_mask * dS).sum(axis=0, keepdims=True))
+    return out, g
+
+
+# ----------------------------------------------------------------------------
 # Optimiser
 # ----------------------------------------------------------------------------
 

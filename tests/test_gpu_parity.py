@@ -119,3 +119,40 @@ def test_duplicated_batch_gives_same_gradients():
     for name, off, shape in net.param_layout():
         n = int(np.prod(shape))
         assert rel_err(g2[off:off + n], g1[off:off + n]) < 1e-4, name
+
+
+def test_phased_reductions_match_single_pass(monkeypatch):
+    """The multi-GPU reduction path (per-rank phase-1 sums -> all-reduce ->
+    phase-2 finish, lcn_api.cpp bn_stats / bn_back) forced on one GPU, where
+    the all-reduce is the identity, must reproduce the single-pass path."""
+    cfg, params, x, lab, net = _setup(dict(F=64, L=2, knn=3), 300)
+    loss0, _ = net.train_step(x, lab, update=False, keep_grads=True)
+    g0 = net.get_grads()
+    out0 = net.forward(x)
+    monkeypatch.setenv("LCN_FORCE_PHASED", "1")
+    net2 = make_network(cfg, max_batch=300)
+    net2.set_params(O.flatten(cfg, params))
+    loss1, _ = net2.train_step(x, lab, update=False, keep_grads=True)
+    g1 = net2.get_grads()
+    np.testing.assert_allclose(net2.forward(x), out0, rtol=0, atol=1e-6)
+    assert loss1 == pytest.approx(loss0, rel=1e-6)
+    for name, off, shape in net.param_layout():
+        n = int(np.prod(shape))
+        assert rel_err(g1[off:off + n], g0[off:off + n]) < 1e-6, name
+
+
+def test_full_size_cfg3_matches_oracle():
+    """BASELINE.json configs[1] at its full size (B = 65 536, F = 64, L = 3,
+    knn = 3): outputs and every gradient against the float64 oracle."""
+    B = 65536
+    cfg, params, x, lab, net = _setup(dict(F=64, L=3, knn=3), B, seed=4)
+    out = net.forward(x)
+    loss, _ = net.train_step(x, lab, update=False, keep_grads=True)
+    g = O.unflatten(cfg, net.get_grads())
+    out64, cache = O.forward(cfg, params, x, np.float64)
+    assert np.abs(out - out64).max() <= 1e-4
+    assert abs(loss - (O.mse_loss(out64, lab) + O.reg_loss(cfg, params))) <= 1e-5 * abs(loss)
+    ref = O.backward(cfg, params, cache, lab, np.float64)
+    del cache
+    bad = {k: rel_err(g[k], ref[k]) for k, _ in O.param_specs(cfg) if rel_err(g[k], ref[k]) > 1e-4}
+    assert not bad, bad
