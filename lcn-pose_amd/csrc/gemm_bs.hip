@@ -22,8 +22,10 @@
 // Workgroup = 4 waves = 4 row tiles (128 rows) x one output slab.  Each wave
 // loads its own activation fragments straight from HBM/L2 into registers (8
 // coalesced 1 KB loads per input slab, prefetched one slab ahead in a second
-// register set); the weight block, shared by the 4 waves, goes through LDS
-// in a double buffer, so there is one barrier per input slab.  Measured
+// register set); the weight block, shared by the 4 waves, goes into a double
+// LDS buffer by LDS-DMA, so there is one barrier per input slab.  The
+// accumulators start at bias + residual, and the BN-backward epilogue's z is
+// fetched at kernel start, so no epilogue operand load is exposed.  Measured
 // against a 128x64 LDS-staged tile with two barriers per slab: 124 vs 114
 // TFLOP/s at cfg3.
 //
@@ -54,16 +56,16 @@ namespace lcn {
     P##0 = xs_[0]; P##1 = xs_[64]; P##2 = xs_[128]; P##3 = xs_[192];      \
     P##4 = xs_[256]; P##5 = xs_[320]; P##6 = xs_[384]; P##7 = xs_[448];   \
   }
-// this thread's quarter of a weight block, global -> registers -> LDS
-#define LOADW(BLK)                                                        \
+// this thread's quarter of a weight block, global -> LDS buffer BUF by
+// LDS-DMA (global_load_lds_dwordx4: no VGPRs, no ds_write; each wave
+// instruction lands 1 KB lane-linear, which is the fragment-packed order)
+#define GLDS(SRC, DST) \
+  __builtin_amdgcn_global_load_lds((const void*)(SRC), (__attribute__((address_space(3))) void*)(DST), 16, 0, 0);
+#define LOADW(BLK, BUF)                                                   \
   {                                                                       \
     const float4* ws_ = W4 + (size_t)(BLK) * 1024 + threadIdx.x;          \
-    st0 = ws_[0]; st1 = ws_[256]; st2 = ws_[512]; st3 = ws_[768];         \
-  }
-#define STOREW(BUF)                                                       \
-  {                                                                       \
-    float4* d_ = Wl + (BUF) * 1024 + threadIdx.x;                         \
-    d_[0] = st0; d_[256] = st1; d_[512] = st2; d_[768] = st3;             \
+    float4* d_ = Wl + (BUF) * 1024 + (threadIdx.x & ~63);                 \
+    GLDS(ws_, d_) GLDS(ws_ + 256, d_ + 256) GLDS(ws_ + 512, d_ + 512) GLDS(ws_ + 768, d_ + 768) \
   }
 #define GSTEP(BUF, G, XV, CH)                                             \
   {                                                                       \
@@ -118,45 +120,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   const int spj = a.spj_in;
   constexpr int DSR = PRO == PRO_BNACT ? 4 : 2;  // LDS reads per k-group
 
-  f32x16 acc0, acc1;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) { acc0[k] = 0.f; acc1[k] = 0.f; }
-  float4 st0, st1, st2, st3;
-  DECLX(xa)
-  DECLX(xb)
-  int2 ia = idx[beg], ib = ia;
-  LOADW(ia.y)
-  LOADX(xa, ia.x)
-  STOREW(0)
-  __syncthreads();
-  // every output slab has >= 1 input block (checked in lcn_create)
-  for (int e = beg; e < end; e += 2) {
-    const bool n1 = e + 1 < end;
-    if (n1) {
-      ib = idx[e + 1];
-      LOADW(ib.y)
-      LOADX(xb, ib.x)
-    }
-    COMPX(0, xa, (ia.x % spj) * kSlab)
-    if (n1) STOREW(1)
-    __syncthreads();
-    if (n1) {
-      const bool n2 = e + 2 < end;
-      if (n2) {
-        ia = idx[e + 2];
-        LOADW(ia.y)
-        LOADX(xa, ia.x)
-      }
-      COMPX(1, xb, (ib.x % spj) * kSlab)
-      if (n2) STOREW(0)
-      __syncthreads();
-    }
-  }
-
-  // ---- epilogue ----
+  // accumulators start at bias + residual (the MFMAs add onto them)
   const int S_out = a.S_out, ncols = S_out * kSlab;
   const size_t tbase = ((size_t)rt * S_out + so) * 512 + lane;  // float4 index of chunk 0
-  float v[32];
+  f32x16 acc0, acc1;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
@@ -170,15 +137,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
       b0.x += r0.x; b0.y += r0.y; b0.z += r0.z; b0.w += r0.w;
       b1.x += r1.x; b1.y += r1.y; b1.z += r1.z; b1.w += r1.w;
     }
-    v[4 * q + 0] = acc0[4 * q + 0] + b0.x;
-    v[4 * q + 1] = acc0[4 * q + 1] + b0.y;
-    v[4 * q + 2] = acc0[4 * q + 2] + b0.z;
-    v[4 * q + 3] = acc0[4 * q + 3] + b0.w;
-    v[16 + 4 * q + 0] = acc1[4 * q + 0] + b1.x;
-    v[16 + 4 * q + 1] = acc1[4 * q + 1] + b1.y;
-    v[16 + 4 * q + 2] = acc1[4 * q + 2] + b1.z;
-    v[16 + 4 * q + 3] = acc1[4 * q + 3] + b1.w;
+    acc0[4 * q + 0] = b0.x; acc0[4 * q + 1] = b0.y; acc0[4 * q + 2] = b0.z; acc0[4 * q + 3] = b0.w;
+    acc1[4 * q + 0] = b1.x; acc1[4 * q + 1] = b1.y; acc1[4 * q + 2] = b1.z; acc1[4 * q + 3] = b1.w;
   }
+  // EPI_BNBACK reads z of the layer below: fetched now, used after the loop;
+  // the per-channel BN constants of this output slab go to an LDS table
+  float4 zp0, zp1, zp2, zp3, zp4, zp5, zp6, zp7;
+  float* ptab = (float*)(Wl + 2048);  // [4][64]: scale, shift, mean, rstd
+  if constexpr (EPI == EPI_BNBACK) {
+    const float4* Z4 = (const float4*)a.epi_z + tbase;
+    zp0 = Z4[0]; zp1 = Z4[64]; zp2 = Z4[128]; zp3 = Z4[192];
+    zp4 = Z4[256]; zp5 = Z4[320]; zp6 = Z4[384]; zp7 = Z4[448];
+    const int pk = threadIdx.x >> 6, ch = (so % (a.epi_F / kSlab)) * kSlab + lane;
+    const float* src = pk == 0 ? a.epi_scale : pk == 1 ? a.epi_shift : pk == 2 ? a.epi_mean : a.epi_rstd;
+    ptab[threadIdx.x] = src[ch];
+  }
+  DECLX(xa)
+  DECLX(xb)
+  int2 ia = idx[beg], ib = ia;
+  LOADW(ia.y, 0)
+  LOADX(xa, ia.x)
+  __syncthreads();
+  // every output slab has >= 1 input block (checked in lcn_create)
+  for (int e = beg; e < end; e += 2) {
+    const bool n1 = e + 1 < end;
+    if (n1) {
+      ib = idx[e + 1];
+      LOADW(ib.y, 1)
+      LOADX(xb, ib.x)
+    }
+    COMPX(0, xa, (ia.x % spj) * kSlab)
+    __syncthreads();  // drains the LDS-DMA of buffer 1 (vmcnt(0)) and publishes it
+    if (n1) {
+      const bool n2 = e + 2 < end;
+      if (n2) {
+        ia = idx[e + 2];
+        LOADW(ia.y, 0)
+        LOADX(xa, ia.x)
+      }
+      COMPX(1, xb, (ib.x % spj) * kSlab)
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue ----
+  float v[32];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { v[k] = acc0[k]; v[16 + k] = acc1[k]; }
   if (live) {
     float4* Y = (float4*)a.Y;
 #pragma unroll
@@ -223,38 +228,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
     return;
   }
   // EPI_BNBACK: du = dh * leaky'(u(z)), zhat = (z - mean) * rstd of the layer
-  // below; pass 0 reduces du, pass 1 du * zhat (z re-read from L2)
-  const int chb = (so % (a.epi_F / kSlab)) * kSlab + 4 * h;
-  const float4* Z4 = (const float4*)a.epi_z;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {  // chunk q holds values 4q..4q+3 (acc0 for q < 4, acc1 after)
-    const float4 z4 = Z4[tbase + q * 64];
-    const int ch = chb + 8 * q;
-    const float4 sc = *(const float4*)(a.epi_scale + ch), sh = *(const float4*)(a.epi_shift + ch);
-    v[4 * q + 0] = fmaf(z4.x, sc.x, sh.x) > 0.f ? v[4 * q + 0] : v[4 * q + 0] * al;
-    v[4 * q + 1] = fmaf(z4.y, sc.y, sh.y) > 0.f ? v[4 * q + 1] : v[4 * q + 1] * al;
-    v[4 * q + 2] = fmaf(z4.z, sc.z, sh.z) > 0.f ? v[4 * q + 2] : v[4 * q + 2] * al;
-    v[4 * q + 3] = fmaf(z4.w, sc.w, sh.w) > 0.f ? v[4 * q + 3] : v[4 * q + 3] * al;
-    put(q, v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-    __builtin_amdgcn_sched_barrier(0);  // one chunk's loads at a time (register pressure)
+  // below; pass 0 reduces du, pass 1 du * zhat
+#define BNBACK_EPI(P)                                                                      \
+  {                                                                                        \
+    const float4 zq[8] = {P##0, P##1, P##2, P##3, P##4, P##5, P##6, P##7};                 \
+    _Pragma("unroll") for (int q = 0; q < 8; ++q) {                                        \
+      const float4 z4 = zq[q];                                                             \
+      const int ch = 8 * q + 4 * h;                                                        \
+      const float4 sc = *(const float4*)(ptab + ch), sh = *(const float4*)(ptab + 64 + ch); \
+      v[4 * q + 0] = fmaf(z4.x, sc.x, sh.x) > 0.f ? v[4 * q + 0] : v[4 * q + 0] * al;      \
+      v[4 * q + 1] = fmaf(z4.y, sc.y, sh.y) > 0.f ? v[4 * q + 1] : v[4 * q + 1] * al;      \
+      v[4 * q + 2] = fmaf(z4.z, sc.z, sh.z) > 0.f ? v[4 * q + 2] : v[4 * q + 2] * al;      \
+      v[4 * q + 3] = fmaf(z4.w, sc.w, sh.w) > 0.f ? v[4 * q + 3] : v[4 * q + 3] * al;      \
+      put(q, v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);                          \
+    }                                                                                      \
+    __syncthreads();                                                                       \
+    for (int r = 0; r < n; ++r) P_ += get(r);                                              \
+    __syncthreads();                                                                       \
+    _Pragma("unroll") for (int q = 0; q < 8; ++q) {                                        \
+      const float4 z4 = zq[q];                                                             \
+      const int ch = 8 * q + 4 * h;                                                        \
+      const float4 mu = *(const float4*)(ptab + 128 + ch), rs = *(const float4*)(ptab + 192 + ch); \
+      put(q, v[4 * q] * ((z4.x - mu.x) * rs.x), v[4 * q + 1] * ((z4.y - mu.y) * rs.y),     \
+          v[4 * q + 2] * ((z4.z - mu.z) * rs.z), v[4 * q + 3] * ((z4.w - mu.w) * rs.w));   \
+    }                                                                                      \
+    __syncthreads();                                                                       \
+    for (int r = 0; r < n; ++r) Q_ += get(r);                                              \
   }
-  __syncthreads();
-  float P = 0.f;
-  for (int r = 0; r < n; ++r) P += get(r);
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const float4 z4 = Z4[tbase + q * 64];
-    const int ch = chb + 8 * q;
-    const float4 mu = *(const float4*)(a.epi_mean + ch), rs = *(const float4*)(a.epi_rstd + ch);
-    put(q, v[4 * q] * ((z4.x - mu.x) * rs.x), v[4 * q + 1] * ((z4.y - mu.y) * rs.y),
-        v[4 * q + 2] * ((z4.z - mu.z) * rs.z), v[4 * q + 3] * ((z4.w - mu.w) * rs.w));
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  __syncthreads();
-  float Q = 0.f;
-  for (int r = 0; r < n; ++r) Q += get(r);
-  if (live) *stat = make_float2(P, Q);
+  float P_ = 0.f, Q_ = 0.f;
+  BNBACK_EPI(zp)
+#undef BNBACK_EPI
+  if (live) *stat = make_float2(P_, Q_);
 }
 
 void launch_gemm_bs(const GemmArgs& a, hipStream_t s) {
@@ -267,7 +271,7 @@ void launch_gemm_bs(const GemmArgs& a, hipStream_t s) {
     else LAUNCH(PRO_BNACT, EPI_NONE, ldsp);
   } else {
     if (a.epi_mode == EPI_BNFWD) LAUNCH(PRO_RAW, EPI_BNFWD, lds);
-    else if (a.epi_mode == EPI_BNBACK) LAUNCH(PRO_RAW, EPI_BNBACK, lds);
+    else if (a.epi_mode == EPI_BNBACK) LAUNCH(PRO_RAW, EPI_BNBACK, lds + 256 * sizeof(float));
     else LAUNCH(PRO_RAW, EPI_NONE, lds);
   }
 #undef LAUNCH
