@@ -180,6 +180,19 @@ def main():
     barrier()
     tfwd = float(net.allreduce_host([time.perf_counter() - tf0], op="max")[0])
 
+    # PCIe-inclusive rate: the same step fed from host (pageable) arrays, as
+    # cgcnn.fit does per step (H2D copy of x and labels + step + sync)
+    for _ in range(1):
+        net.train_step(x, lab, want_loss=False)
+    barrier()
+    th0 = time.perf_counter()
+    nh = max(3, args.steps // 2)
+    for _ in range(nh):
+        net.train_step(x, lab, want_loss=False)
+    net.synchronize()
+    barrier()
+    thost = float(net.allreduce_host([time.perf_counter() - th0], op="max")[0])
+
     ms_step = elapsed / args.steps * 1e3
     value = B * world * args.steps / elapsed
     if rank == 0:
@@ -208,6 +221,7 @@ def main():
             "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv for kk, vv in v.items()}
                         for k, v in kern.items()},
             "fwd_only_poses_per_s": round(B * world * nf / tfwd, 1),
+            "host_input_poses_per_s": round(B * world * nh / thost, 1),
         }
         if args.cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
