@@ -162,10 +162,16 @@ int main(int argc, char** argv) {
   d.d_shift = sh;
   d.d_c123 = c123;
   d.d_F = F;
-  std::vector<int> hwr(nblk, 0), seen(J, 0);
-  for (int b = 0; b < nblk; ++b)
-    if (!seen[blk[b].y]) { seen[blk[b].y] = 1; hwr[b] = 1; }
-  d.dz_writer = dev(hwr);
+  std::vector<int4> grp;  // as lcn_api.cpp upload_dw_groups
+  for (int so = 0; so < J; ++so) {
+    std::vector<int> ids;
+    for (int b = 0; b < nblk; ++b)
+      if (blk[b].y == so) ids.push_back(b);
+    for (size_t i = 0; i < ids.size(); i += 2)
+      grp.push_back(make_int4(so, ids[i], i + 1 < ids.size() ? ids[i + 1] : -1, i == 0 ? 1 : 0));
+  }
+  d.groups = dev(grp);
+  d.ngroups = (int)grp.size();
   float* dzo;
   CK(hipMalloc(&dzo, (size_t)B * H * 4));
   d.dz_out = dzo;

@@ -8,152 +8,172 @@
 
 namespace lcn {
 
-// One workgroup = one 64x64 block (si, so) x one batch chunk; 4 waves in a
-// 2x2 grid of 32x32 MFMA tiles; 64 batch rows (two row tiles) per LDS stage.
-// Work ids are chunk-major so the blocks of one chunk (same batch rows) run
-// on one XCD and share the activation tiles through its L2.
+// One workgroup = a group of up to two 64x64 blocks (si0, so), (si1, so) x
+// one batch chunk; waves (bi, hp) = (w >> 1, w & 1) compute rows 32hp..+31 of
+// block bi against all 64 columns (two 32x32 accumulators), so the staged D
+// slab -- and its BN-backward rebuild -- serves both blocks.  One 32-row tile
+// per LDS stage.  Work ids are chunk-major so the groups of one chunk (same
+// batch rows) run on one XCD and share the activation tiles through its L2.
 //
-// Staging: every thread loads 4 float4 of each operand's two 8 KB row-tile
-// slabs (coalesced 1 KB chunks), applies the operand transform, and scatters
-// them transposed into LDS ([feature][row], row stride 68 floats: the scatter
-// and the ds_read_b128 fragment reads are both bank-conflict free).  The MFMA
-// runs over the batch: lane l supplies A[b][p = l&31] and D[b][q = l&31] for
-// k = b, four consecutive rows per float4 (lane half h takes rows 8g + 4h + s).
+// Staging: every thread loads 2 float4 of each operand's 8 KB row-tile slab
+// (coalesced 1 KB chunks), applies the operand transform (channel constants
+// from small LDS tables), and scatters them transposed into LDS as
+// [feature][row] with row stride 36 floats: the ds_write_b32 scatter and the
+// ds_read_b128 fragment reads (lane l reads feature l & 31, rows 8g + 4h ..
+// +3) are both bank-conflict free.  The MFMA runs over the batch: k = row.
 //
 // PRO: the A operand gets BN apply + LeakyReLU (A = z of the layer below the
 // block's inner layer); DBB: the D operand is dz rebuilt from (dh, z) by the
-// BN + LeakyReLU backward, dz = c1 du + c2 + c3 z; the workgroups of one
-// designated block per output slab also store that dz (dz_out) for the
-// backward-data GEMM that follows, so dz costs one write and no separate
-// elementwise pass.
-constexpr int kDwLd = 68;
+// BN + LeakyReLU backward, dz = c1 du + c2 + c3 z; one group per output slab
+// also stores that dz (dz_out) for the backward-data GEMM that follows, so dz
+// costs one write and no separate elementwise pass.
+constexpr int kDwLd = 36;
 
 template <bool PRO, bool DBB>
-__global__ __launch_bounds__(256) void gemm_dw_kernel(GemmDwArgs a) {
-  __shared__ __attribute__((aligned(16))) float As[64 * kDwLd];  // [p][row]
-  __shared__ __attribute__((aligned(16))) float Ds[64 * kDwLd];  // [q][row]
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gemm_dw_kernel(GemmDwArgs a) {
+  __shared__ __attribute__((aligned(16))) float Ds[64 * kDwLd];      // [q][row]
+  __shared__ __attribute__((aligned(16))) float As[2][64 * kDwLd];   // [p][row] per block
+  // channel constants: A sc, sh of si0; A sc, sh of si1; D sc, sh, c1, c2, c3
+  __shared__ __attribute__((aligned(16))) float tab[9 * 64];
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int chunk = wg / a.nblk, b = wg - chunk * a.nblk;
-  const int2 sb = a.blk[b];
+  const int chunk = wg / a.ngroups, gi = wg - chunk * a.ngroups;
+  const int4 grp = a.groups[gi];
+  const int so = grp.x, b0 = grp.y, b1 = grp.z;
+  const bool two = b1 >= 0;
+  const int si0 = a.blk[b0].x, si1 = two ? a.blk[b1].x : si0;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int lr = lane & 31, h = lane >> 5;
-  const int wp = w >> 1, wq = w & 1;
+  const int bi = w >> 1, hp = w & 1;
+  const bool wave_live = bi == 0 || two;
   const int r0 = chunk * a.chunk_rows;
   const int r1 = min(a.B, r0 + a.chunk_rows);
-  const int last_rt = (a.B + kRT - 1) / kRT - 1;
-  const bool writer = DBB && a.dz_out && a.dz_writer[b];
+  const bool writer = DBB && a.dz_out && grp.w;
 
-  f32x16 acc;
+  {
+    const int c = t & 63, k = t >> 6;  // 4 x 64 entries per pass
+    if constexpr (PRO) {
+      const int ch0 = (si0 % a.spj_a) * kSlab + c, ch1 = (si1 % a.spj_a) * kSlab + c;
+      tab[t] = k == 0 ? a.pro_scale[ch0] : k == 1 ? a.pro_shift[ch0] : k == 2 ? a.pro_scale[ch1] : a.pro_shift[ch1];
+    }
+    if constexpr (DBB) {
+      const int ch = (so % a.spj_d) * kSlab + c, F = a.d_F;
+      tab[256 + t] = k == 0 ? a.d_scale[ch] : k == 1 ? a.d_shift[ch] : k == 2 ? a.d_c123[ch] : a.d_c123[F + ch];
+      if (k == 0) tab[512 + c] = a.d_c123[2 * F + ch];
+    }
+  }
+
+  f32x16 acc0, acc1;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) acc[k] = 0.f;
+  for (int k = 0; k < 16; ++k) { acc0[k] = 0.f; acc1[k] = 0.f; }
 
-  // this thread's staging slots: j = 0..3 -> row tile j >> 1 of the stage,
-  // chunk g = w + 4 (j & 1), lane `lane`: features 8g + 4h .. +3
-  float4 sc0 = make_float4(1.f, 1.f, 1.f, 1.f), sh0 = make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 sc1 = sc0, sh1 = sh0;
-  if constexpr (PRO) {
-    const int ch = (sb.x % a.spj_a) * kSlab + 8 * w + 4 * h;
-    sc0 = *(const float4*)(a.pro_scale + ch);
-    sh0 = *(const float4*)(a.pro_shift + ch);
-    sc1 = *(const float4*)(a.pro_scale + ch + 32);
-    sh1 = *(const float4*)(a.pro_shift + ch + 32);
-  }
-  BnBackCoef cf0{}, cf1{};
-  if constexpr (DBB) {
-    const int ch = (sb.y % a.spj_d) * kSlab + 8 * w + 4 * h;
-    cf0 = load_bnback_coef(a.d_scale, a.d_shift, a.d_c123, a.d_F, ch);
-    cf1 = load_bnback_coef(a.d_scale, a.d_shift, a.d_c123, a.d_F, ch + 32);
-  }
+  // this thread's staging slots: j = 0, 1 -> chunk g = w + 4j of the stage's
+  // row tile, lane `lane`: row lr, features f0 + 32j .. +3
   const float4* A4 = (const float4*)a.A;
   const float4* D4 = (const float4*)a.D;
   const float4* Z4 = (const float4*)a.d_z;
   const int S_a = a.S_a, S_d = a.S_d;
-  const int c40 = t, c41 = t + 256;  // chunk-local float4 index of j even / odd
-  float4 ra0, ra1, ra2, ra3, rd0, rd1, rd2, rd3, rz0, rz1, rz2, rz3;
-  // float4 index of (row tile, chunk-local index) in a tiled operand with S slabs at slab sl
+  const int c40 = t, c41 = t + 256;
+  const int f0 = 8 * w + 4 * h;
+  float4 ra0, ra1, rb0, rb1, rd0, rd1, rz0, rz1;
 #define DW_IX(RT, S, SL, C4) (((size_t)(RT) * (S) + (SL)) * 512 + (C4))
-#define DW_GLOAD(BASE)                                                            \
-  {                                                                               \
-    const int t0_ = min((BASE) / kRT, last_rt), t1_ = min((BASE) / kRT + 1, last_rt); \
-    ra0 = A4[DW_IX(t0_, S_a, sb.x, c40)];                                         \
-    ra1 = A4[DW_IX(t0_, S_a, sb.x, c41)];                                         \
-    ra2 = A4[DW_IX(t1_, S_a, sb.x, c40)];                                         \
-    ra3 = A4[DW_IX(t1_, S_a, sb.x, c41)];                                         \
-    rd0 = D4[DW_IX(t0_, S_d, sb.y, c40)];                                         \
-    rd1 = D4[DW_IX(t0_, S_d, sb.y, c41)];                                         \
-    rd2 = D4[DW_IX(t1_, S_d, sb.y, c40)];                                         \
-    rd3 = D4[DW_IX(t1_, S_d, sb.y, c41)];                                         \
-    if constexpr (DBB) {                                                          \
-      rz0 = Z4[DW_IX(t0_, S_d, sb.y, c40)];                                       \
-      rz1 = Z4[DW_IX(t0_, S_d, sb.y, c41)];                                       \
-      rz2 = Z4[DW_IX(t1_, S_d, sb.y, c40)];                                       \
-      rz3 = Z4[DW_IX(t1_, S_d, sb.y, c41)];                                       \
-    }                                                                             \
+#define DW_GLOAD(BASE)                                                     \
+  {                                                                        \
+    const int t_ = (BASE) / kRT;                                           \
+    ra0 = A4[DW_IX(t_, S_a, si0, c40)];                                    \
+    ra1 = A4[DW_IX(t_, S_a, si0, c41)];                                    \
+    if (two) {                                                             \
+      rb0 = A4[DW_IX(t_, S_a, si1, c40)];                                  \
+      rb1 = A4[DW_IX(t_, S_a, si1, c41)];                                  \
+    }                                                                      \
+    rd0 = D4[DW_IX(t_, S_d, so, c40)];                                     \
+    rd1 = D4[DW_IX(t_, S_d, so, c41)];                                     \
+    if constexpr (DBB) {                                                   \
+      rz0 = Z4[DW_IX(t_, S_d, so, c40)];                                   \
+      rz1 = Z4[DW_IX(t_, S_d, so, c41)];                                   \
+    }                                                                      \
   }
   if (r0 < r1) DW_GLOAD(r0);
-  for (int base = r0; base < r1; base += 64) {
-    __syncthreads();
-    const bool v0 = base + lr < r1, v1 = base + 32 + lr < r1;  // row of tile 0 / 1 valid
+  for (int base = r0; base < r1; base += kRT) {
+    __syncthreads();  // previous stage's fragment reads are done (and the tables written)
+    const bool v = base + lr < r1;
     if constexpr (PRO) {
-      ra0 = bnact4(ra0, sc0, sh0, a.alpha); ra1 = bnact4(ra1, sc1, sh1, a.alpha);
-      ra2 = bnact4(ra2, sc0, sh0, a.alpha); ra3 = bnact4(ra3, sc1, sh1, a.alpha);
-    }
-    if constexpr (DBB) {
-      rd0 = bnback4(rd0, rz0, cf0, a.alpha); rd1 = bnback4(rd1, rz1, cf1, a.alpha);
-      rd2 = bnback4(rd2, rz2, cf0, a.alpha); rd3 = bnback4(rd3, rz3, cf1, a.alpha);
-      if (writer) {
-        float4* o = (float4*)a.dz_out;
-        const int t0 = base / kRT;
-        if (v0) { o[DW_IX(t0, S_d, sb.y, c40)] = rd0; o[DW_IX(t0, S_d, sb.y, c41)] = rd1; }
-        if (v1) { o[DW_IX(t0 + 1, S_d, sb.y, c40)] = rd2; o[DW_IX(t0 + 1, S_d, sb.y, c41)] = rd3; }
+      ra0 = bnact4(ra0, *(const float4*)(tab + f0), *(const float4*)(tab + 64 + f0), a.alpha);
+      ra1 = bnact4(ra1, *(const float4*)(tab + f0 + 32), *(const float4*)(tab + 96 + f0), a.alpha);
+      if (two) {
+        rb0 = bnact4(rb0, *(const float4*)(tab + 128 + f0), *(const float4*)(tab + 192 + f0), a.alpha);
+        rb1 = bnact4(rb1, *(const float4*)(tab + 160 + f0), *(const float4*)(tab + 224 + f0), a.alpha);
       }
     }
-    {
-      // rows past the chunk end contribute nothing (both operands zeroed)
+    if constexpr (DBB) {
+      auto coef = [&](int f) {
+        BnBackCoef c;
+        c.sc = *(const float4*)(tab + 256 + f); c.sh = *(const float4*)(tab + 320 + f);
+        c.c1 = *(const float4*)(tab + 384 + f); c.c2 = *(const float4*)(tab + 448 + f);
+        c.c3 = *(const float4*)(tab + 512 + f);
+        return c;
+      };
+      rd0 = bnback4(rd0, rz0, coef(f0), a.alpha);
+      rd1 = bnback4(rd1, rz1, coef(f0 + 32), a.alpha);
+      if (writer && v) {
+        float4* o = (float4*)a.dz_out;
+        const int t_ = base / kRT;
+        o[DW_IX(t_, S_d, so, c40)] = rd0;
+        o[DW_IX(t_, S_d, so, c41)] = rd1;
+      }
+    }
+    if (!v) {  // rows past the chunk end contribute nothing
       const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!v0) { ra0 = z4; ra1 = z4; rd0 = z4; rd1 = z4; }
-      if (!v1) { ra2 = z4; ra3 = z4; rd2 = z4; rd3 = z4; }
+      ra0 = z4; ra1 = z4; rb0 = z4; rb1 = z4; rd0 = z4; rd1 = z4;
     }
     {
-      // transposed scatter: feature 8g + 4h + s -> LDS row, batch row -> column
-      const int f0 = 8 * w + 4 * h;  // j even (g = w); j odd adds 32 (g = w + 4)
-      float* a0 = As + f0 * kDwLd + lr;
-      float* d0 = Ds + f0 * kDwLd + lr;
-#define DW_PUT(P, F4, COL)                 \
-  P[(COL)] = (F4).x;                       \
-  P[(COL) + kDwLd] = (F4).y;               \
-  P[(COL) + 2 * kDwLd] = (F4).z;           \
-  P[(COL) + 3 * kDwLd] = (F4).w;
-      DW_PUT(a0, ra0, 0) DW_PUT(a0, ra1, 32 * kDwLd) DW_PUT(a0, ra2, 32) DW_PUT(a0, ra3, 32 * kDwLd + 32)
-      DW_PUT(d0, rd0, 0) DW_PUT(d0, rd1, 32 * kDwLd) DW_PUT(d0, rd2, 32) DW_PUT(d0, rd3, 32 * kDwLd + 32)
+      // transposed scatter: feature -> LDS row, batch row -> column
+#define DW_PUT(P, F4, OFF)             \
+  P[(OFF)] = (F4).x;                   \
+  P[(OFF) + kDwLd] = (F4).y;           \
+  P[(OFF) + 2 * kDwLd] = (F4).z;       \
+  P[(OFF) + 3 * kDwLd] = (F4).w;
+      const int o0 = f0 * kDwLd + lr, o1 = o0 + 32 * kDwLd;
+      DW_PUT(As[0], ra0, o0) DW_PUT(As[0], ra1, o1)
+      if (two) { DW_PUT(As[1], rb0, o0) DW_PUT(As[1], rb1, o1) }
+      DW_PUT(Ds, rd0, o0) DW_PUT(Ds, rd1, o1)
 #undef DW_PUT
     }
     __syncthreads();
-    if (base + 64 < r1) DW_GLOAD(base + 64);
-    const float* Ap = As + (32 * wp + lr) * kDwLd + 4 * h;
-    const float* Dp = Ds + (32 * wq + lr) * kDwLd + 4 * h;
+    if (base + kRT < r1) DW_GLOAD(base + kRT);
+    if (wave_live) {
+      const float* Ap = As[bi] + (32 * hp + lr) * kDwLd + 4 * h;
+      const float* D0 = Ds + lr * kDwLd + 4 * h;
+      const float* D1 = Ds + (32 + lr) * kDwLd + 4 * h;
 #pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      const float4 av = *(const float4*)(Ap + 8 * g);
-      const float4 dv = *(const float4*)(Dp + 8 * g);
-      acc = MFMA32(av.x, dv.x, acc);
-      acc = MFMA32(av.y, dv.y, acc);
-      acc = MFMA32(av.z, dv.z, acc);
-      acc = MFMA32(av.w, dv.w, acc);
+      for (int g = 0; g < 4; ++g) {
+        const float4 av = *(const float4*)(Ap + 8 * g);
+        const float4 d0 = *(const float4*)(D0 + 8 * g);
+        const float4 d1 = *(const float4*)(D1 + 8 * g);
+        acc0 = MFMA32(av.x, d0.x, acc0);
+        acc1 = MFMA32(av.x, d1.x, acc1);
+        acc0 = MFMA32(av.y, d0.y, acc0);
+        acc1 = MFMA32(av.y, d1.y, acc1);
+        acc0 = MFMA32(av.z, d0.z, acc0);
+        acc1 = MFMA32(av.z, d1.z, acc1);
+        acc0 = MFMA32(av.w, d0.w, acc0);
+        acc1 = MFMA32(av.w, d1.w, acc1);
+      }
     }
   }
 #undef DW_GLOAD
 #undef DW_IX
-  float* out = a.part + ((size_t)chunk * a.nblk + b) * 4096;
+  if (!wave_live) return;
+  float* out = a.part + ((size_t)chunk * a.nblk + (bi ? b1 : b0)) * 4096;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const int p = 32 * wp + (k & 3) + 8 * (k >> 2) + 4 * h;
-    out[p * 64 + 32 * wq + lr] = acc[k];
+    const int p = 32 * hp + (k & 3) + 8 * (k >> 2) + 4 * h;
+    out[p * 64 + lr] = acc0[k];
+    out[p * 64 + 32 + lr] = acc1[k];
   }
 }
 
 void launch_gemm_dw(const GemmDwArgs& a, hipStream_t s) {
-  const int grid = a.nblk * a.nchunks;
+  const int grid = a.ngroups * a.nchunks;
   const bool pro = a.pro_scale != nullptr, dbb = a.d_bnback != 0;
   if (pro && dbb)
     hipLaunchKernelGGL((gemm_dw_kernel<true, true>), dim3(grid), dim3(256), 0, s, a);

@@ -89,7 +89,9 @@ struct Handle {
   // DH: gradient w.r.t. a block output h_l; DG: w.r.t. the inner activation g;
   // DZ: dz of a hidden layer, stored by its weight-gradient GEMM
   float *DH = nullptr, *DG = nullptr, *DZ = nullptr;
-  int* dz_writer = nullptr;       // per hidden block: 1 for the first block of each output slab
+  // weight-gradient work groups (kernels_gemm.hip): up to 2 blocks sharing an output slab
+  int4 *grp_hidden = nullptr, *grp_lift = nullptr, *grp_out = nullptr;
+  int ngrp_hidden = 0, ngrp_lift = 0, ngrp_out = 0;
   std::vector<BnStats> bn;
   std::vector<double*> zsum;      // per BN layer: column sums of z (bias-gradient term)
   float *ident_scale = nullptr, *ident_shift = nullptr, *ident_c123 = nullptr;
@@ -175,6 +177,23 @@ int upload(Handle* h, T** p, const std::vector<T>& src) {
 }
 
 int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Pair the blocks of each output slab into weight-gradient work groups
+// (so, block0, block1 | -1, stores dz): the first group of a slab stores dz.
+int upload_dw_groups(Handle* h, const std::vector<int2>& blk, int4** dev, int* n) {
+  int nso = 0;
+  for (const int2& b : blk) nso = std::max(nso, b.y + 1);
+  std::vector<int4> g;
+  for (int so = 0; so < nso; ++so) {
+    std::vector<int> ids;
+    for (size_t b = 0; b < blk.size(); ++b)
+      if (blk[b].y == so) ids.push_back((int)b);
+    for (size_t i = 0; i < ids.size(); i += 2)
+      g.push_back(make_int4(so, ids[i], i + 1 < ids.size() ? ids[i + 1] : -1, i == 0 ? 1 : 0));
+  }
+  *n = (int)g.size();
+  return upload(h, dev, g);
+}
 
 // batch chunks of the weight-gradient GEMM: ~8k workgroups in total, <= 64 chunks
 int dw_chunks(int nblk) { return std::max(1, std::min(64, 8192 / std::max(1, nblk))); }
@@ -277,10 +296,7 @@ int build(Handle* h, const lcn_config* c) {
     bptr.push_back((int)bidx.size());
   }
   CHECK(upload(h, &h->blk, blk));
-  std::vector<int> writer(blk.size(), 0), seen(h->nslab, 0);
-  for (size_t b = 0; b < blk.size(); ++b)
-    if (!seen[blk[b].y]) { seen[blk[b].y] = 1; writer[b] = 1; }
-  CHECK(upload(h, &h->dz_writer, writer));
+  CHECK(upload_dw_groups(h, blk, &h->grp_hidden, &h->ngrp_hidden));
   CHECK(upload(h, &h->fwd_ptr, fptr));
   CHECK(upload(h, &h->bwd_ptr, bptr));
   CHECK(upload(h, &h->fwd_idx, fidx));
@@ -309,6 +325,8 @@ int build(Handle* h, const lcn_config* c) {
   CHECK(upload(h, &h->out_idx, oidx));
   CHECK(upload(h, &h->lift_blk, lblk));
   CHECK(upload(h, &h->out_blk, oblk));
+  CHECK(upload_dw_groups(h, lblk, &h->grp_lift, &h->ngrp_lift));
+  CHECK(upload_dw_groups(h, oblk, &h->grp_out, &h->ngrp_out));
 
   // ---- per-layer weight forms ----
   for (int k = 0; k < nl; ++k) {
@@ -594,17 +612,16 @@ int gemm_dw(Handle* h, const Operand& A, const Operand& D, const int2* blk, int 
     a.d_c123 = h->batch_norm ? h->c123 : h->ident_c123;
     a.d_F = h->F;
     a.dz_out = dz_out;
-    a.dz_writer = h->dz_writer;
-    if (dz_out && blk != h->blk) {
-      h->err = "internal: dz store needs the hidden block list";
-      return LCN_E_ARG;
-    }
   }
   a.spj_a = h->spj;
   a.spj_d = h->spj;
   a.alpha = h->alpha;
   a.blk = blk;
   a.nblk = nblk;
+  if (blk == h->blk) { a.groups = h->grp_hidden; a.ngroups = h->ngrp_hidden; }
+  else if (blk == h->lift_blk) { a.groups = h->grp_lift; a.ngroups = h->ngrp_lift; }
+  else if (blk == h->out_blk) { a.groups = h->grp_out; a.ngroups = h->ngrp_out; }
+  else { h->err = "internal: unknown block list"; return LCN_E_ARG; }
   a.B = B;
   const int nch = std::max(1, std::min<int>(dw_chunks(nblk), (int)cdiv(B, 64)));
   a.chunk_rows = (int)(cdiv(cdiv(B, nch), 64) * 64);

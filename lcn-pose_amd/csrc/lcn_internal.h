@@ -78,16 +78,18 @@ struct GemmArgs {
 void launch_gemm_bs(const GemmArgs& a, hipStream_t s);
 
 // dWe blocks: part[chunk][blk][p][q] = sum_{b in chunk} A[b, si*64+p] * D[b, so*64+q]
+// Work unit = a group of up to 2 blocks with the same output slab so (they
+// share the staged D operand): int4 (so, block0, block1 or -1, stores dz).
 struct GemmDwArgs {
   const float* A; int S_a;           // tiled
   const float* D; int S_d;           // tiled; d_bnback: D = dh and the operand is dz
   const float* pro_scale; const float* pro_shift; int spj_a; float alpha;  // A: BN apply + act
   int d_bnback; int spj_d;
   const float* d_z; const float* d_scale; const float* d_shift; const float* d_c123; int d_F;
-  const int* dz_writer;              // d_bnback: per block, 1 if it stores dz (one per so)
   float* dz_out;                     // d_bnback: dz (tiled like D) or null
   const int2* blk;                   // (si, so) per block
   int nblk;
+  const int4* groups; int ngroups;   // block groups (see above)
   int B; int chunk_rows; int nchunks;  // chunk_rows: multiple of 64
   float* part;                       // [nchunks][nblk][4096]
 };
