@@ -31,9 +31,12 @@
 //
 // Operand prologue (PRO):  PRO_RAW a = X;  PRO_BNACT a = leaky(scale X + shift)
 // (BN apply + LeakyReLU of the input's layer, scale/shift tables in LDS).
-// Epilogue: + bias / + residual, store; then per 32-row tile either BN forward
-// partials of the output (sum, M2 about the tile mean) or BN backward partials
-// of the layer below (sum du, sum du * zhat), column sums through LDS.
+// Epilogue: store; then per 128-row group either BN forward partials of the
+// output (sum, M2 about the group mean) or BN backward partials of the layer
+// below (sum du, sum du * zhat): column sums per wave through LDS, merged
+// across the 4 waves.
+#include <algorithm>
+
 #include "gemm_common.h"
 
 namespace lcn {
@@ -202,7 +205,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   float* red = (float*)Wl + w * 2048;
   const int c = lane, cg = c >> 3, chh = (c >> 2) & 1, cs = c & 3;
   const int n = live ? min(kRT, a.B - rt * kRT) : 0;  // valid rows of the tile
-  float2* stat = a.stat + (size_t)rt * ncols + so * kSlab + c;
+  // the 4 waves' column partials are merged into one per 128-row group
+  float* comb = (float*)(Wl + 2048) + 256;  // [4 waves][64 columns][3]
+  float2* stat = a.stat + (size_t)rtg * ncols + so * kSlab + c;
   auto put = [&](int q, float x0, float x1, float x2, float x3) {
     const int pos = lane ^ (2 * q + h);
     *(float4*)(red + (q * 64 + pos) * 4) = make_float4(x0, x1, x2, x3);
@@ -224,7 +229,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
       const float d = get(r) - mean;
       m2 = fmaf(d, d, m2);
     }
-    if (live) *stat = make_float2(sum, m2);
+    comb[(w * 64 + c) * 3 + 0] = sum;
+    comb[(w * 64 + c) * 3 + 1] = m2;
+    comb[(w * 64 + c) * 3 + 2] = (float)n;
+    __syncthreads();
+    if (w == 0) {  // Chan et al. merge of the 4 row tiles: (sum, M2 about the group mean)
+      float S = 0.f, N = 0.f;
+#pragma unroll
+      for (int i = 0; i < kGemmWaves; ++i) {
+        S += comb[(i * 64 + c) * 3 + 0];
+        N += comb[(i * 64 + c) * 3 + 2];
+      }
+      const float mu = S / N;
+      float M2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < kGemmWaves; ++i) {
+        const float ni = comb[(i * 64 + c) * 3 + 2];
+        if (ni > 0.f) {
+          const float d = comb[(i * 64 + c) * 3 + 0] / ni - mu;
+          M2 += comb[(i * 64 + c) * 3 + 1] + ni * d * d;
+        }
+      }
+      *stat = make_float2(S, M2);
+    }
     return;
   }
   // EPI_BNBACK: du = dh * leaky'(u(z)), zhat = (z - mean) * rstd of the layer
@@ -258,20 +285,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   float P_ = 0.f, Q_ = 0.f;
   BNBACK_EPI(zp)
 #undef BNBACK_EPI
-  if (live) *stat = make_float2(P_, Q_);
+  comb[(w * 64 + c) * 3 + 0] = P_;
+  comb[(w * 64 + c) * 3 + 1] = Q_;
+  __syncthreads();
+  if (w == 0) {
+    float P = 0.f, Q = 0.f;
+#pragma unroll
+    for (int i = 0; i < kGemmWaves; ++i) {
+      P += comb[(i * 64 + c) * 3 + 0];
+      Q += comb[(i * 64 + c) * 3 + 1];
+    }
+    *stat = make_float2(P, Q);
+  }
 }
 
 void launch_gemm_bs(const GemmArgs& a, hipStream_t s) {
   const int grid = ((a.n_rt + kGemmWaves - 1) / kGemmWaves) * a.n_out_slabs;
+  // weight double buffer; BN tables / epilogue constants and the 4-wave merge after it
   const size_t lds = 2 * 1024 * sizeof(float4);
-  const size_t ldsp = lds + 2 * a.pro_F * sizeof(float);
+  const size_t ldse = lds + (256 + 4 * 64 * 3) * sizeof(float);
+  const size_t ldsp = std::max(lds + 2 * a.pro_F * sizeof(float), ldse);
 #define LAUNCH(P, E, L) hipLaunchKernelGGL((gemm_bs_kernel<P, E>), dim3(grid), dim3(256), L, s, a)
   if (a.pro_mode == PRO_BNACT) {
     if (a.epi_mode == EPI_BNFWD) LAUNCH(PRO_BNACT, EPI_BNFWD, ldsp);
     else LAUNCH(PRO_BNACT, EPI_NONE, ldsp);
   } else {
-    if (a.epi_mode == EPI_BNFWD) LAUNCH(PRO_RAW, EPI_BNFWD, lds);
-    else if (a.epi_mode == EPI_BNBACK) LAUNCH(PRO_RAW, EPI_BNBACK, lds + 256 * sizeof(float));
+    if (a.epi_mode == EPI_BNFWD) LAUNCH(PRO_RAW, EPI_BNFWD, ldse);
+    else if (a.epi_mode == EPI_BNBACK) LAUNCH(PRO_RAW, EPI_BNBACK, ldse);
     else LAUNCH(PRO_RAW, EPI_NONE, lds);
   }
 #undef LAUNCH

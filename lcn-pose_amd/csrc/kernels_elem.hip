@@ -4,7 +4,7 @@
 // variance, tf.nn.batch_normalization's x*inv + (beta - mean*inv)),
 // tf.nn.leaky_relu(alpha=0.2) and the residual add (models_att.py:704).
 //
-// Statistics are reduced in three levels: per 32-row tile the producing
+// Statistics are reduced in three levels: per 128-row group the producing
 // GEMM's epilogue writes (sum, sum of squared deviations about the tile mean)
 // -- or, backward, (sum du, sum du*zhat) -- as float; colreduce merges the
 // tiles of every column in float64; the channel kernels merge the 17 joint

@@ -439,7 +439,7 @@ int build(Handle* h, const lcn_config* c) {
     }
   }
   CHECK(dalloc(h, &h->c123, 3 * F));
-  CHECK(dalloc(h, &h->stat_part, (size_t)cdiv(B, kRT) * H));
+  CHECK(dalloc(h, &h->stat_part, (size_t)cdiv(B, kGemmRows) * H));
   CHECK(dalloc(h, &h->col_part, (size_t)cdiv(B, kEwRows) * 64));
   CHECK(dalloc(h, &h->colacc, (size_t)kColSplit * H));
   h->loss_grid = (int)std::min<int64_t>(2048, cdiv(B, 4));
@@ -496,7 +496,7 @@ int bn_stats(Handle* h, int k, int B) {
   const double count = (double)B * h->world * kJ;
   const float* gamma = h->theta + h->gamma_off[k];
   const float* beta = h->theta + h->beta_off[k];
-  launch_colreduce(h->stat_part, (int)cdiv(B, kRT), kRT, B, h->H, 1, h->colacc, s);
+  launch_colreduce(h->stat_part, (int)cdiv(B, kGemmRows), kGemmRows, B, h->H, 1, h->colacc, s);
   if (!h->phased && h->world == 1) {
     launch_bn_fwd_finalize(h->colacc, h->H, h->F, 0, count, gamma, beta, h->eps, h->acc1, h->bn[k],
                            h->zsum[k], s);
@@ -648,7 +648,7 @@ int bn_back(Handle* h, int k, int B) {
   float* dgam = bn ? h->rg + h->gamma_off[k] : nullptr;
   float* dbet = bn ? h->rg + h->beta_off[k] : nullptr;
   float* db = h->rg + h->b_off[k];
-  launch_colreduce(h->stat_part, (int)cdiv(B, kRT), kRT, B, h->H, 0, h->colacc, s);
+  launch_colreduce(h->stat_part, (int)cdiv(B, kGemmRows), kGemmRows, B, h->H, 0, h->colacc, s);
   if ((!h->phased && h->world == 1) || !bn) {
     launch_bn_bwd_finalize(h->colacc, h->H, h->F, 0, bn, count, (double)B, gamma, st.mean, st.rstd,
                            h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);

@@ -10,6 +10,7 @@ constexpr int kJ = 17;          // joints (models_att.py:512-513)
 constexpr int kSlab = 64;       // feature slab = MFMA tile edge; F is a multiple of it
 constexpr int kRT = 32;         // rows per row tile of the activation layout
 constexpr int kGemmWaves = 4;   // row tiles (one per wave) per block-sparse GEMM workgroup
+constexpr int kGemmRows = kRT * kGemmWaves;  // rows per workgroup = per BN partial
 constexpr int kEwRows = 256;    // rows per tile of the output-bias column partials
 
 // ----------------------------------------------------------------------------
@@ -49,7 +50,7 @@ __host__ __device__ inline int frag_ix(int n, int k) {
 // operand transform applied while staging: raw, BN apply + LeakyReLU, or (the
 // weight-gradient kernel's D operand) the BN + LeakyReLU backward dz from dh, z
 enum { PRO_RAW = 0, PRO_BNACT = 1, PRO_BNBACK = 2 };
-// epilogue partials per 32-row tile: EPI_BNFWD = BN statistics of the output
+// epilogue partials per 128-row group: EPI_BNFWD = BN statistics of the output
 // (sum, M2 about the tile mean); EPI_BNBACK = BN-backward sums of the layer
 // below (sum du, sum du*zhat)
 enum { EPI_NONE = 0, EPI_BNFWD = 1, EPI_BNBACK = 2 };
@@ -69,7 +70,7 @@ struct GemmArgs {
   float* Y; int S_out;               // output (tiled, S_out slabs)
   const float* addsrc;               // Y = acc (+ addsrc), tiled like Y; may alias Y
   int epi_mode;
-  float2* stat;                      // partials [n_rt][S_out*64]
+  float2* stat;                      // partials [ceil(n_rt / 4)][S_out*64]
   const float* epi_z;                // EPI_BNBACK: z of the layer below (tiled like Y)
   const float* epi_scale; const float* epi_shift; const float* epi_mean; const float* epi_rstd;
   int epi_F;                         // channels of the epi_* vectors (spj of Y = epi_F/64)

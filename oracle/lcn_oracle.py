@@ -419,8 +419,8 @@ def backward(cfg: Config, params, cache, lab: np.ndarray, dtype=np.float32,
 # Data-parallel decomposition (SyncBN), as liblcn runs it with world > 1
 # ----------------------------------------------------------------------------
 
-def _tile_moments(z3: np.ndarray, tile_rows: int = 32):
-    """Per-channel (sum z, sum (M2_t + s_t^2 / n_t)) over the 32-row tiles of a
+def _tile_moments(z3: np.ndarray, tile_rows: int = 128):
+    """Per-channel (sum z, sum (M2_t + s_t^2 / n_t)) over the 128-row groups of a
     shard -- the float64 quantities bn_fwd_finalize all-reduces
     (lcn-pose_amd/csrc/kernels_elem.hip colreduce mode 1)."""
     B, _, F = z3.shape

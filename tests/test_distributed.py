@@ -1,6 +1,6 @@
 """Data-parallel decomposition (world > 1) on CPU over gloo.
 
-liblcn runs a multi-GPU step as: per-rank 32-row tile moments of every BN
+liblcn runs a multi-GPU step as: per-rank 128-row tile moments of every BN
 layer -> RCCL all-reduce (float64) -> SyncBN statistics; per-rank BN-backward
 sums -> all-reduce -> dz coefficients; LOCAL raw gradients (dW_e, db, dgamma,
 dbeta with the global-batch loss scale) -> one all-reduce of the raw-gradient
