@@ -115,6 +115,52 @@ int lcn_device_buffer(void* handle, int32_t slot, int64_t bytes, void** dptr);
 int lcn_memcpy_h2d(void* handle, void* dst, const void* src, int64_t bytes);
 int lcn_memcpy_d2h(void* handle, void* dst, const void* src, int64_t bytes);
 
+/* --- device-resident datasets --------------------- */
+/* The reference feeds every step from host numpy arrays: fit() fancy-indexes
+ * the float64 train arrays with a permutation deque (models_att.py:193-212),
+ * predict() slices fixed zero-padded batches (:88-121), inference.py
+ * concatenates augmented copies before predict and undoes them after it
+ * (inference.py:70-110, tools/data.py:10-54, 205-322).  These entry points keep
+ * the arrays in HBM (in the caller's dtype; float64 is cast to float32 on the
+ * device exactly as a float32 feed would) and build every batch there. */
+enum { LCN_DTYPE_F32 = 0, LCN_DTYPE_F64 = 1 };
+enum { LCN_MAX_DATASETS = 16, LCN_MAX_COPIES = 8 };
+/* augmentation op per copy of the virtually concatenated dataset */
+enum {
+  LCN_AUG_NONE = 0,       /* identity                                           */
+  LCN_AUG_FLIP = 1,       /* flip_data (data.py:10-25) / unflip_data (:236-249) */
+  LCN_AUG_ROTATE = 2,     /* rotate_data (data.py:289-322): param0 = cos, param1 = sin of the angle,
+                             computed by the caller as numpy does (np.cos(np.radians(a)))        */
+  LCN_AUG_TRANSLATE = 3   /* translation_data (data.py:27-54): param0 = +t; as undo
+                             (untranslation_data :205-218, all three coordinates): param0 = t */
+};
+typedef struct lcn_augment {
+  int32_t n_copies;               /* 1 + number of augmentations                */
+  int32_t op[LCN_MAX_COPIES];     /* op of copy c (copy 0 is normally NONE)      */
+  double param0[LCN_MAX_COPIES];
+  double param1[LCN_MAX_COPIES];
+} lcn_augment;
+/* copy rows x cols (row-major, dtype LCN_DTYPE_*) into dataset `slot` on the device */
+int lcn_dataset_upload(void* handle, int32_t slot, const void* data, int32_t dtype, int64_t rows,
+                       int32_t cols);
+int lcn_dataset_free(void* handle, int32_t slot);
+/* fit's step (models_att.py:194-212) on rows idx[0..B) of datasets x_slot
+ * ([N][17*in_F]) and lab_slot ([N][51]); idx is host memory, or device memory
+ * with LCN_IN_DEVICE.  Same flags / outputs as lcn_train_step. */
+int lcn_train_step_indexed(void* handle, int32_t x_slot, int32_t lab_slot, const int32_t* idx,
+                           int64_t batch, int32_t flags, float* loss_out, float* lr_out);
+/* predict (models_att.py:79-132) over the whole dataset x_slot, virtually
+ * concatenated as aug->n_copies augmented copies (aug NULL = one plain copy):
+ * fixed batches of batch_size, the last zero-padded, batch-statistics BN.
+ * With more than one copy the predictions are undone per copy by `undo` and
+ * averaged (data.undo).  out: host float64 [N][51].  lab_slot >= 0 (no
+ * augmentation): batch_losses[i] receives batch i's float32 mean loss
+ * (losses_cap >= number of batches).  With world > 1 every rank predicts its
+ * own shard and the ranks' batch i together form one SyncBN batch. */
+int lcn_predict_dataset(void* handle, int32_t x_slot, int32_t lab_slot, int64_t batch_size,
+                        const lcn_augment* aug, const lcn_augment* undo, double* out,
+                        float* batch_losses, int64_t losses_cap, int64_t* n_batches);
+
 /* --- data parallel (RCCL over xGMI) ------------------------------------ */
 int lcn_comm_unique_id(void* id_out /* 128 bytes */);
 int lcn_comm_init(void* handle, const void* id /* 128 bytes */, int32_t rank, int32_t world);
@@ -127,7 +173,9 @@ int lcn_set_timing(void* handle, int32_t enable);
 int lcn_kernel_timing(void* handle, int32_t kernel, int64_t* launches, double* total_ms,
                       double* flops);
 /* debug: copy an internal activation to host.  kind 0 = z (pre-BN) of linear
- * layer idx, 1 = block output h_idx, 2 = BN (mean, rstd) of BN layer idx */
+ * layer idx, 1 = block output h_idx, 2 = BN (mean, rstd) of BN layer idx,
+ * 3 = output [B][51], 4 = raw gradient vector, 5 = the batch's input x
+ * [B][17*in_F] as the lift layer sees it, 6 = the batch's labels [B][51] */
 int lcn_debug_tensor(void* handle, int32_t kind, int32_t idx, float* host, int64_t n);
 
 #ifdef __cplusplus

@@ -116,6 +116,15 @@ struct Handle {
   std::vector<void*> user_bufs;
   std::vector<int64_t> user_bytes;
 
+  // device-resident datasets (lcn_dataset_upload) and the predict scratch
+  struct Dataset { void* ptr = nullptr; int dtype = 0; int64_t rows = 0; int cols = 0; };
+  std::vector<Dataset> datasets;
+  int* idx_dev = nullptr;         // [Bmax] batch indices
+  double* pred = nullptr;         // [pred_rows][51] float64 predictions of predict_dataset
+  double* pred_out = nullptr;     // [pred_rows][51] undone + averaged
+  float* batch_losses = nullptr;  // [loss_cap] per-batch predict losses
+  int64_t pred_rows = 0, loss_cap = 0;
+
   // communication
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
@@ -405,6 +414,7 @@ int build(Handle* h, const lcn_config* c) {
   const size_t t1 = (size_t)tiled_floats(B, 1), tH = (size_t)tiled_floats(B, h->nslab);
   CHECK(dalloc(h, &h->x, t1));
   CHECK(dalloc(h, &h->xin, (size_t)B * kJ * h->inF));
+  CHECK(dalloc(h, &h->idx_dev, (size_t)B));
   CHECK(dalloc(h, &h->lab, (size_t)B * 51));
   CHECK(dalloc(h, &h->out, (size_t)B * 51));
   CHECK(dalloc(h, &h->dy, t1));
@@ -855,6 +865,10 @@ int lcn_destroy(void* handle) {
     for (auto e : t.ev) hipEventDestroy(e);
   for (void* p : h->allocs) hipFree(p);
   for (void* p : h->user_bufs) if (p) hipFree(p);
+  for (auto& d : h->datasets) if (d.ptr) hipFree(d.ptr);
+  if (h->pred) hipFree(h->pred);
+  if (h->pred_out) hipFree(h->pred_out);
+  if (h->batch_losses) hipFree(h->batch_losses);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return LCN_OK;
@@ -989,12 +1003,7 @@ int lcn_forward_loss(void* handle, const float* x, const float* labels, float* o
   return LCN_OK;
 }
 
-int lcn_train_step(void* handle, const float* x, const float* labels, int64_t B, int32_t flags,
-                   float* loss_out, float* lr_out) {
-  Handle* h = (Handle*)handle;
-  if (!h || !x || !labels) return LCN_E_ARG;
-  HIPC(hipSetDevice(h->device));
-  CHECK(stage_inputs(h, x, labels, B, flags));
+static int run_train_step(Handle* h, int64_t B, int32_t flags, float* loss_out, float* lr_out) {
   const float lr = h->lr0 * powf(h->decay_rate, (float)h->global_step / (float)h->decay_steps);
   CHECK(forward(h, (int)B, true, true));
   if (h->world > 1) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
@@ -1004,6 +1013,197 @@ int lcn_train_step(void* handle, const float* x, const float* labels, int64_t B,
   if (lr_out) *lr_out = lr;
   CHECK(read_loss(h, B, loss_out));
   if (!(flags & LCN_ASYNC)) HIPC(hipStreamSynchronize(h->stream));
+  return LCN_OK;
+}
+
+int lcn_train_step(void* handle, const float* x, const float* labels, int64_t B, int32_t flags,
+                   float* loss_out, float* lr_out) {
+  Handle* h = (Handle*)handle;
+  if (!h || !x || !labels) return LCN_E_ARG;
+  HIPC(hipSetDevice(h->device));
+  CHECK(stage_inputs(h, x, labels, B, flags));
+  return run_train_step(h, B, flags, loss_out, lr_out);
+}
+
+// ---------------------------------------------------------------------------
+// device-resident datasets
+// ---------------------------------------------------------------------------
+static int dataset_of(Handle* h, int32_t slot, Handle::Dataset** d) {
+  if (slot < 0 || slot >= (int)h->datasets.size() || !h->datasets[slot].ptr) {
+    h->err = "dataset slot " + std::to_string(slot) + " is empty (lcn_dataset_upload)";
+    return LCN_E_ARG;
+  }
+  *d = &h->datasets[slot];
+  return LCN_OK;
+}
+
+static int check_augment(Handle* h, const lcn_augment* a, Augment* out) {
+  std::memset(out, 0, sizeof(*out));
+  out->n_copies = 1;
+  if (!a) return LCN_OK;
+  if (a->n_copies < 1 || a->n_copies > LCN_MAX_COPIES) {
+    h->err = "augment n_copies must be in [1, " + std::to_string(LCN_MAX_COPIES) + "]";
+    return LCN_E_ARG;
+  }
+  out->n_copies = a->n_copies;
+  for (int c = 0; c < a->n_copies; ++c) {
+    if (a->op[c] < LCN_AUG_NONE || a->op[c] > LCN_AUG_TRANSLATE) {
+      h->err = "unknown augment op " + std::to_string(a->op[c]);
+      return LCN_E_ARG;
+    }
+    out->op[c] = a->op[c];
+    out->p0[c] = a->param0[c];
+    out->p1[c] = a->param1[c];
+  }
+  return LCN_OK;
+}
+
+int lcn_dataset_upload(void* handle, int32_t slot, const void* data, int32_t dtype, int64_t rows,
+                       int32_t cols) {
+  Handle* h = (Handle*)handle;
+  if (!h || !data || slot < 0 || slot >= LCN_MAX_DATASETS || rows <= 0 || cols <= 0 ||
+      (dtype != LCN_DTYPE_F32 && dtype != LCN_DTYPE_F64))
+    return LCN_E_ARG;
+  if (rows > (int64_t)INT32_MAX) { h->err = "dataset rows must fit int32 indices"; return LCN_E_ARG; }
+  HIPC(hipSetDevice(h->device));
+  HIPC(hipStreamSynchronize(h->stream));
+  if ((int)h->datasets.size() <= slot) h->datasets.resize(slot + 1);
+  Handle::Dataset& d = h->datasets[slot];
+  const size_t bytes = (size_t)rows * cols * (dtype == LCN_DTYPE_F64 ? 8 : 4);
+  if (d.ptr) { hipFree(d.ptr); d = Handle::Dataset(); }
+  if (hipMalloc(&d.ptr, bytes) != hipSuccess) {
+    d.ptr = nullptr;
+    h->err = "hipMalloc dataset (" + std::to_string(bytes) + " bytes)";
+    return LCN_E_NOMEM;
+  }
+  HIPC(hipMemcpy(d.ptr, data, bytes, hipMemcpyHostToDevice));
+  d.dtype = dtype;
+  d.rows = rows;
+  d.cols = cols;
+  return LCN_OK;
+}
+
+int lcn_dataset_free(void* handle, int32_t slot) {
+  Handle* h = (Handle*)handle;
+  if (!h) return LCN_E_ARG;
+  if (slot < 0 || slot >= (int)h->datasets.size() || !h->datasets[slot].ptr) return LCN_OK;
+  HIPC(hipSetDevice(h->device));
+  HIPC(hipStreamSynchronize(h->stream));
+  hipFree(h->datasets[slot].ptr);
+  h->datasets[slot] = Handle::Dataset();
+  return LCN_OK;
+}
+
+// build the batch (x tiles, labels) from dataset rows on the device
+static int gather_batch(Handle* h, Handle::Dataset* dx, Handle::Dataset* dl, const int* idx_dev,
+                        int64_t base, const Augment& aug, int64_t B) {
+  launch_gather_x(dx->ptr, dx->dtype, dx->rows, h->inF, idx_dev, base, aug, (int)B, h->x, h->stream);
+  if (dl) launch_gather_rows(dl->ptr, dl->dtype, dl->rows, 51, idx_dev, base, (int)B, h->lab, h->stream);
+  h->lastB = B;
+  return LCN_OK;
+}
+
+int lcn_train_step_indexed(void* handle, int32_t x_slot, int32_t lab_slot, const int32_t* idx,
+                           int64_t B, int32_t flags, float* loss_out, float* lr_out) {
+  Handle* h = (Handle*)handle;
+  if (!h || !idx) return LCN_E_ARG;
+  HIPC(hipSetDevice(h->device));
+  Handle::Dataset *dx = nullptr, *dl = nullptr;
+  CHECK(dataset_of(h, x_slot, &dx));
+  CHECK(dataset_of(h, lab_slot, &dl));
+  if (dx->cols != kJ * h->inF || dl->cols != 51 || dl->rows != dx->rows) {
+    h->err = "dataset shapes: x must be [N][17*in_F], labels [N][51]";
+    return LCN_E_ARG;
+  }
+  if (B <= 0 || B > h->Bmax) { h->err = "batch outside [1, max_batch]"; return LCN_E_ARG; }
+  const int* id = (const int*)idx;
+  if (!(flags & LCN_IN_DEVICE)) {
+    HIPC(hipMemcpyAsync(h->idx_dev, idx, (size_t)B * 4, hipMemcpyHostToDevice, h->stream));
+    id = h->idx_dev;
+  }
+  Augment none;
+  CHECK(check_augment(h, nullptr, &none));
+  CHECK(gather_batch(h, dx, dl, id, 0, none, B));
+  return run_train_step(h, B, flags, loss_out, lr_out);
+}
+
+int lcn_predict_dataset(void* handle, int32_t x_slot, int32_t lab_slot, int64_t batch_size,
+                        const lcn_augment* aug, const lcn_augment* undo, double* out,
+                        float* batch_losses, int64_t losses_cap, int64_t* n_batches) {
+  Handle* h = (Handle*)handle;
+  if (!h || !out) return LCN_E_ARG;
+  HIPC(hipSetDevice(h->device));
+  Handle::Dataset *dx = nullptr, *dl = nullptr;
+  CHECK(dataset_of(h, x_slot, &dx));
+  if (lab_slot >= 0) CHECK(dataset_of(h, lab_slot, &dl));
+  if (dx->cols != kJ * h->inF) { h->err = "x dataset must be [N][17*in_F]"; return LCN_E_ARG; }
+  if (batch_size <= 0 || batch_size > h->Bmax) { h->err = "batch_size outside [1, max_batch]"; return LCN_E_ARG; }
+  Augment a, u;
+  CHECK(check_augment(h, aug, &a));
+  CHECK(check_augment(h, undo, &u));
+  if (u.n_copies != a.n_copies) { h->err = "augment / undo copy counts differ"; return LCN_E_ARG; }
+  if (dl && (a.n_copies != 1 || dl->cols != 51 || dl->rows != dx->rows)) {
+    h->err = "labels need [N][51] and no augmentation";
+    return LCN_E_ARG;
+  }
+  const int64_t N = dx->rows, total = N * a.n_copies;
+  int64_t nb = cdiv(total, batch_size);
+  if (h->world > 1) {  // every rank runs the same number of (SyncBN) batches
+    double v = (double)nb;
+    CHECK(lcn_comm_allreduce_host(h, &v, 1, 1));
+    nb = (int64_t)v;
+  }
+  if (h->pred_rows < total) {
+    HIPC(hipStreamSynchronize(h->stream));
+    if (h->pred) hipFree(h->pred);
+    if (h->pred_out) hipFree(h->pred_out);
+    h->pred = nullptr;
+    h->pred_out = nullptr;
+    h->pred_rows = 0;
+    if (hipMalloc(&h->pred, (size_t)total * 51 * 8) != hipSuccess ||
+        hipMalloc(&h->pred_out, (size_t)total * 51 * 8) != hipSuccess) {
+      h->err = "hipMalloc predictions";
+      return LCN_E_NOMEM;
+    }
+    h->pred_rows = total;
+  }
+  if (batch_losses && dl && nb > losses_cap) {
+    h->err = "batch_losses holds " + std::to_string(losses_cap) + " < " + std::to_string(nb) + " batches";
+    return LCN_E_ARG;
+  }
+  if (h->loss_cap < nb) {
+    HIPC(hipStreamSynchronize(h->stream));
+    if (h->batch_losses) hipFree(h->batch_losses);
+    h->batch_losses = nullptr;
+    h->loss_cap = 0;
+    if (hipMalloc(&h->batch_losses, (size_t)nb * 4) != hipSuccess) { h->err = "hipMalloc losses"; return LCN_E_NOMEM; }
+    h->loss_cap = nb;
+  }
+  // models_att.py:88-121: fixed batches over the (virtually concatenated)
+  // copies, zero-padded last batch, batch-statistics BN
+  for (int64_t i = 0; i < nb; ++i) {
+    const int64_t begin = i * batch_size;
+    CHECK(gather_batch(h, dx, dl, nullptr, begin, a, batch_size));
+    CHECK(forward(h, (int)batch_size, dl != nullptr, false));
+    if (dl) {
+      if (h->world > 1) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
+      launch_batch_loss(h->loss_sum, (double)batch_size * h->world * 51.0, h->batch_losses, (int)i,
+                        h->stream);
+    }
+    const int64_t n = std::min<int64_t>(batch_size, total - begin);
+    if (n > 0) launch_store_pred(h->out, n, h->pred + begin * 51, h->stream);
+  }
+  const double* res = h->pred;
+  if (a.n_copies > 1) {  // data.undo (data.py:269-287)
+    launch_tta_undo(h->pred, N, u, h->pred_out, h->stream);
+    res = h->pred_out;
+  }
+  CHECK(finish_launches(h));
+  HIPC(hipMemcpyAsync(out, res, (size_t)N * 51 * 8, hipMemcpyDeviceToHost, h->stream));
+  if (batch_losses && dl && nb > 0)
+    HIPC(hipMemcpyAsync(batch_losses, h->batch_losses, (size_t)nb * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(hipStreamSynchronize(h->stream));
+  if (n_batches) *n_batches = nb;
   return LCN_OK;
 }
 
@@ -1137,6 +1337,15 @@ int lcn_debug_tensor(void* handle, int32_t kind, int32_t idx, float* host, int64
     HIPC(hipMemcpy(host + h->F, h->bn[idx].rstd, h->F * 4, hipMemcpyDeviceToHost));
     return LCN_OK;
   } else if (kind == 3) { src = h->out; cnt = h->lastB * 51; }
+  else if (kind == 5) {  // the lift operand x (1-slab row tiles) -> row-major [B][17*in_F]
+    const int cols = kJ * h->inF;
+    if (n < h->lastB * cols) { h->err = "buffer too small"; return LCN_E_ARG; }
+    std::vector<float> t((size_t)tiled_floats(h->lastB, 1));
+    HIPC(hipMemcpy(t.data(), h->x, t.size() * 4, hipMemcpyDeviceToHost));
+    for (int64_t b = 0; b < h->lastB; ++b)
+      for (int c = 0; c < cols; ++c) host[b * cols + c] = t[tix(b, c, 1)];
+    return LCN_OK;
+  } else if (kind == 6) { src = h->lab; cnt = h->lastB * 51; }
   else if (kind == 4) { src = h->rg; cnt = h->P; }
   else return LCN_E_ARG;
   if (n < cnt) { h->err = "buffer too small"; return LCN_E_ARG; }

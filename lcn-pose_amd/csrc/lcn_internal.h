@@ -125,6 +125,31 @@ struct OutAsmArgs {
 void launch_out_assemble(const OutAsmArgs& a, int grid, hipStream_t s);
 
 // ----------------------------------------------------------------------------
+// Device-resident datasets (kernels_data.hip): permutation gather into the
+// lift operand, test-time augmentation copies and their undo + mean.
+// ----------------------------------------------------------------------------
+enum { kF32 = 0, kF64 = 1 };
+enum { kAugNone = 0, kAugFlip = 1, kAugRotate = 2, kAugTranslate = 3 };
+constexpr int kMaxCopies = 8;
+// copies of the virtual dataset: op / parameters per copy (rotate: p0 = cos,
+// p1 = sin of the angle; translate: p0 = t)
+struct Augment {
+  int n_copies;
+  int op[kMaxCopies];
+  double p0[kMaxCopies], p1[kMaxCopies];
+};
+// x rows v = idx[b] (or base + b) of the augmented dataset [rows][17*k] ->
+// 1-slab row tiles of B rows (zero rows outside the virtual range / past B)
+void launch_gather_x(const void* ds, int dtype, int64_t rows, int k, const int* idx, int64_t base,
+                     const Augment& aug, int B, float* dst, hipStream_t s);
+// rows v = idx[b] (or base + b) of ds [rows][cols] -> float32 row-major [B][cols]
+void launch_gather_rows(const void* ds, int dtype, int64_t rows, int cols, const int* idx,
+                        int64_t base, int B, float* dst, hipStream_t s);
+void launch_store_pred(const float* out, int64_t n, double* pred, hipStream_t s);
+void launch_tta_undo(const double* pred, int64_t N, const Augment& undo, double* out, hipStream_t s);
+void launch_batch_loss(const double* loss_sum, double count, float* losses, int i, hipStream_t s);
+
+// ----------------------------------------------------------------------------
 // BatchNorm (batch statistics), activation, BN backward
 // ----------------------------------------------------------------------------
 // stats per channel: mean, rstd, scale = gamma*rstd, shift = beta - mean*scale

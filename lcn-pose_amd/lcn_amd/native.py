@@ -19,6 +19,9 @@ LCN_ABI_VERSION = 1
 MASK_LOCALLY_CONNECTED, MASK_EXPONENTIAL = 0, 1
 IN_DEVICE, OUT_DEVICE, NO_UPDATE, KEEP_GRADS, ASYNC = 1, 2, 4, 8, 16
 K_GEMM_FWD, K_GEMM_DX, K_GEMM_DW = 0, 1, 2
+DTYPE_F32, DTYPE_F64 = 0, 1
+MAX_DATASETS, MAX_COPIES = 16, 8
+AUG_NONE, AUG_FLIP, AUG_ROTATE, AUG_TRANSLATE = 0, 1, 2, 3
 
 # every entry point include/lcn.h declares, with its ctypes signature
 _i32, _i64, _f32p, _vp = ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_float), ctypes.c_void_p
@@ -34,6 +37,22 @@ class LcnConfig(ctypes.Structure):
                 ("decay_rate", ctypes.c_float), ("beta1", ctypes.c_float),
                 ("beta2", ctypes.c_float), ("adam_eps", ctypes.c_float),
                 ("decay_steps", _i64), ("max_batch", _i64), ("mask_matrix", _f32p)]
+
+
+class LcnAugment(ctypes.Structure):
+    _fields_ = [("n_copies", _i32), ("op", _i32 * MAX_COPIES),
+                ("param0", ctypes.c_double * MAX_COPIES), ("param1", ctypes.c_double * MAX_COPIES)]
+
+
+def make_augment(ops) -> LcnAugment:
+    """ops: list of (op, param0, param1) per copy of the virtual dataset."""
+    a = LcnAugment()
+    if not 1 <= len(ops) <= MAX_COPIES:
+        raise ValueError(f"1..{MAX_COPIES} copies supported, got {len(ops)}")
+    a.n_copies = len(ops)
+    for c, (op, p0, p1) in enumerate(ops):
+        a.op[c], a.param0[c], a.param1[c] = int(op), float(p0), float(p1)
+    return a
 
 
 SIGNATURES = {
@@ -55,6 +74,11 @@ SIGNATURES = {
     "lcn_device_buffer": ([_vp, _i32, _i64, ctypes.POINTER(_vp)], _i32),
     "lcn_memcpy_h2d": ([_vp, _vp, _vp, _i64], _i32),
     "lcn_memcpy_d2h": ([_vp, _vp, _vp, _i64], _i32),
+    "lcn_dataset_upload": ([_vp, _i32, _vp, _i32, _i64, _i32], _i32),
+    "lcn_dataset_free": ([_vp, _i32], _i32),
+    "lcn_train_step_indexed": ([_vp, _i32, _i32, _vp, _i64, _i32, _f32p, _f32p], _i32),
+    "lcn_predict_dataset": ([_vp, _i32, _i32, _i64, ctypes.POINTER(LcnAugment),
+                             ctypes.POINTER(LcnAugment), _f64p, _f32p, _i64, _i64p], _i32),
     "lcn_comm_unique_id": ([_vp], _i32),
     "lcn_comm_init": ([_vp, _vp, _i32, _i32], _i32),
     "lcn_comm_allreduce_host": ([_vp, _f64p, _i32, _i32], _i32),
@@ -253,6 +277,57 @@ class Network:
 
     def device_buffer(self, slot: int, nbytes: int) -> DeviceBuffer:
         return DeviceBuffer(self, slot, nbytes)
+
+    # -- device-resident datasets
+    def dataset_upload(self, slot: int, data: np.ndarray):
+        """Keep `data` ([N][cols], float32 or float64 -- kept as given) in HBM."""
+        a = np.asarray(data)
+        if a.dtype not in (np.float32, np.float64):
+            a = a.astype(np.float64)
+        a = np.ascontiguousarray(a.reshape(a.shape[0], -1))
+        dt = DTYPE_F64 if a.dtype == np.float64 else DTYPE_F32
+        self._check(self.lib.lcn_dataset_upload(self.h, slot, a.ctypes.data, dt, a.shape[0],
+                                                a.shape[1]))
+
+    def dataset_free(self, slot: int):
+        self._check(self.lib.lcn_dataset_free(self.h, slot))
+
+    def train_step_indexed(self, x_slot: int, lab_slot: int, idx, *, update=True,
+                           keep_grads=False, want_loss=True, idx_device_ptr: Optional[int] = None,
+                           batch: Optional[int] = None, sync=True):
+        """fit's step on dataset rows idx (host int array, or a device int32
+        pointer + batch)."""
+        flags = (0 if update else NO_UPDATE) | (KEEP_GRADS if keep_grads else 0)
+        flags |= 0 if sync else ASYNC
+        if idx_device_ptr is not None:
+            ptr, B = idx_device_ptr, int(batch)
+            flags |= IN_DEVICE
+        else:
+            ix = np.ascontiguousarray(idx, dtype=np.int32)
+            ptr, B = ix.ctypes.data, ix.size
+        loss, lr = ctypes.c_float(), ctypes.c_float()
+        self._check(self.lib.lcn_train_step_indexed(
+            self.h, x_slot, lab_slot, ptr, B, flags,
+            ctypes.byref(loss) if (want_loss and sync) else None, ctypes.byref(lr)))
+        return (loss.value if (want_loss and sync) else None), lr.value
+
+    def predict_dataset(self, x_slot: int, n_rows: int, batch_size: int, *, lab_slot: int = -1,
+                        augment=None, undo=None):
+        """predict over a resident dataset; returns float64 [N][51] (and the
+        per-batch float32 losses when lab_slot >= 0)."""
+        out = np.empty((n_rows, 51), np.float64)
+        nb_cap = max(1, -(-n_rows // batch_size)) if lab_slot >= 0 else 0
+        losses = np.zeros(max(nb_cap, 1), np.float32)
+        nb = ctypes.c_int64()
+        a = make_augment(augment) if augment else None
+        u = make_augment(undo) if undo else None
+        self._check(self.lib.lcn_predict_dataset(
+            self.h, x_slot, lab_slot, batch_size, ctypes.byref(a) if a else None,
+            ctypes.byref(u) if u else None, out.ctypes.data_as(_f64p),
+            _fp(losses) if lab_slot >= 0 else None, nb_cap, ctypes.byref(nb)))
+        if lab_slot >= 0:
+            return out, losses[:nb.value]
+        return out
 
     # -- data parallel
     @staticmethod

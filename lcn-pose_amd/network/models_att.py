@@ -14,7 +14,6 @@ Deliberate differences from the reference, all documented in DESIGN.md:
 """
 from __future__ import annotations
 
-import collections
 import json
 import os
 import re
@@ -28,6 +27,9 @@ from lcn_amd.init import init_flat
 from lcn_amd.native import Network
 
 ROOT_PATH = os.path.join(os.path.dirname(os.path.realpath(__file__)), "..")
+# device dataset slots (lcn_dataset_upload): train x / labels, validation x /
+# labels (fit), predict x / labels
+_SLOT_TX, _SLOT_TL, _SLOT_VX, _SLOT_VL, _SLOT_PX, _SLOT_PL = range(6)
 
 # models_att.py:19-36 -- the skeleton edges used for the exponential mask
 _EXP_EDGES = ((0, 1), (0, 7), (0, 4), (4, 5), (4, 7), (5, 6), (1, 7), (1, 2), (2, 3), (7, 11),
@@ -52,6 +54,23 @@ def get_exponential_matrix(verbose=True):
     return exp_mat.astype(np.float32)
 
 
+def permutation_batches(n, batch_size):
+    """Batch indices of fit's loop (models_att.py:193-200): a deque refilled
+    with np.random.permutation(n) whenever fewer than batch_size indices
+    remain, batch_size popped per step -- the same numpy draws in the same
+    order, as array slices instead of per-index popleft()."""
+    pending = np.empty(0, np.int64)
+    head = 0
+    while True:
+        if pending.size - head < batch_size:
+            pending = np.concatenate([pending[head:], np.random.permutation(n)])
+            head = 0
+            if pending.size < batch_size:  # the reference's popleft() runs dry
+                raise IndexError("pop from an empty deque")
+        yield pending[head:head + batch_size]
+        head += batch_size
+
+
 class base_model(object):
     def __init__(self):
         self.regularizers = []
@@ -64,32 +83,47 @@ class base_model(object):
         """Fixed-size batches, zero-padded last batch (models_att.py:79-132).
 
         BatchNorm uses the statistics of each (padded) batch, as the
-        reference graph does."""
-        loss = 0
-        size = data.shape[0]
-        predictions = np.empty((size, self.out_joints * 3))
+        reference graph does.  The data go to HBM once and every batch is
+        built there (lcn_predict_dataset); predictions come back float64."""
         net = self._get_session(sess)
-        bs = self.batch_size
-        batch_data = np.zeros((bs,) + data.shape[1:], np.float32)
-        batch_labels = np.zeros((bs, self.out_joints * 3), np.float32)
-        for begin in range(0, size, bs):
-            end = min(begin + bs, size)
-            tmp = data[begin:end]
-            if not isinstance(tmp, np.ndarray):
-                tmp = tmp.toarray()  # sparse input (models_att.py:95-96)
-            batch_data[:] = 0
-            batch_data[: end - begin] = tmp
-            if labels is not None:
-                batch_labels[:] = 0
-                batch_labels[: end - begin] = labels[begin:end]
-                batch_pred, batch_loss = net.forward_loss(batch_data, batch_labels)
-                loss += batch_loss
-            else:
-                batch_pred = net.forward(batch_data)
-            predictions[begin:end] = batch_pred[: end - begin]
-        if labels is not None:
-            return predictions, loss * bs / size
-        return predictions
+        data = self._dense(data)
+        size = data.shape[0]
+        net.dataset_upload(_SLOT_PX, data)
+        if labels is None:
+            return net.predict_dataset(_SLOT_PX, size, self.batch_size)
+        net.dataset_upload(_SLOT_PL, np.asarray(labels).reshape(size, -1))
+        predictions, losses = net.predict_dataset(_SLOT_PX, size, self.batch_size, lab_slot=_SLOT_PL)
+        return predictions, self._mean_batch_loss(losses, size)
+
+    def predict_tta(self, data, flip=False, rotate=False, translation=None, sess=None):
+        """inference.py:70-110 without the host concatenation: predict the
+        data plus its flipped / rotated (180 degrees) / translated copies and
+        return data.undo's average (tools/data.py:269-287), float64 [N, 51]."""
+        from lcn_amd.tta import augment_ops
+        net = self._get_session(sess)
+        data = self._dense(data)
+        aug, undo, _ = augment_ops(flip=flip, rotate=rotate, translation=translation)
+        net.dataset_upload(_SLOT_PX, data)
+        return net.predict_dataset(_SLOT_PX, data.shape[0], self.batch_size, augment=aug, undo=undo)
+
+    @staticmethod
+    def _dense(data):
+        if not isinstance(data, np.ndarray):
+            data = data.toarray()  # sparse input (models_att.py:95-96)
+        return data.reshape(data.shape[0], -1)
+
+    def _mean_batch_loss(self, losses, size):
+        # `loss += batch_loss` over float32 fetches, then loss * bs / size (:115, :129-130)
+        loss = 0
+        for l in losses:
+            loss += np.float32(l)
+        return loss * self.batch_size / size
+
+    def _evaluate_resident(self, size, net):
+        """evaluate() on the validation set already in HBM (fit's eval step)."""
+        _, losses = net.predict_dataset(_SLOT_VX, size, self.batch_size, lab_slot=_SLOT_VL)
+        loss = self._mean_batch_loss(losses, size)
+        return "loss: {:.4e}".format(loss), loss
 
     def evaluate(self, data, labels, sess=None):
         t_process, t_wall = time.process_time(), time.time()
@@ -127,7 +161,13 @@ class base_model(object):
             ckpt.restore(net, ckpt.latest_checkpoint(starting_checkpoint))
 
         losses = []
-        indices = collections.deque()
+        # the deque of np.random.permutation() indices of :193-200, kept as an
+        # array (same draws, same order); the arrays themselves live in HBM
+        batches = permutation_batches(train_data.shape[0], self.batch_size)
+        net.dataset_upload(_SLOT_TX, train_data)
+        net.dataset_upload(_SLOT_TL, train_labels)
+        net.dataset_upload(_SLOT_VX, self._dense(val_data))
+        net.dataset_upload(_SLOT_VL, np.asarray(val_labels).reshape(val_data.shape[0], -1))
         num_steps = int(self.num_epochs * train_data.shape[0] / self.batch_size)
         eval_frequency = max(1, num_steps // self.num_epochs)
         print(f"Total steps to be done to complete all the epochs: {num_steps}")
@@ -135,11 +175,8 @@ class base_model(object):
         training_error, validation_error = [], []
         loss_average = float("nan")
         for step in range(starting_step, num_steps + 1):
-            if len(indices) < self.batch_size:
-                indices.extend(np.random.permutation(train_data.shape[0]))
-            idx = [indices.popleft() for _ in range(self.batch_size)]
-            batch_data, batch_labels = train_data[idx, ...], train_labels[idx, ...]
-            loss, learning_rate = net.train_step(batch_data, batch_labels)
+            idx = next(batches)
+            loss, learning_rate = net.train_step_indexed(_SLOT_TX, _SLOT_TL, idx)
             loss_average = self._update_loss_average(loss)
 
             if step % eval_frequency == 0:
@@ -149,7 +186,7 @@ class base_model(object):
                 print("  learning_rate = {:.2e}, loss_average = {:.4e}".format(learning_rate,
                                                                                loss_average))
                 training_error.append([time.time(), step, loss_average])
-                string, loss = self.evaluate(val_data, val_labels, net)
+                string, loss = self._evaluate_resident(val_data.shape[0], net)
                 losses.append(loss)
                 print("validation {}".format(string))
                 print("time: {:.0f}s (wall {:.0f}s)".format(time.process_time() - t_process,

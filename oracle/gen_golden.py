@@ -13,8 +13,8 @@ What it pins, and from where:
       imported with an empty ``tensorflow`` placeholder module because the
       module does ``import tensorflow as tf`` at top level and TF is not
       installed (the function itself is pure numpy);
-    - ``tools.data.flip_data / rotate_data / undo`` on seeded inputs
-      (data.py:10-25, 289-322, 269-287), imported with an ``h5py``
+    - ``tools.data.flip_data / rotate_data / translation_data / undo`` on
+      seeded inputs (data.py:10-25, 289-322, 27-54, 269-287), imported with an ``h5py``
       placeholder (data.py:3 imports it and never uses it).
 * ``notebook_masks.npz`` -- the neighbour matrices printed by the reference's
   own Kaggle runs (parameter dumps in kaggle/custom-dataset-h36m.ipynb, knn=2,
@@ -72,6 +72,13 @@ def ref_helpers():
     out["rot_in3"], out["rot_out3"] = x3, data.rotate_data(x3, 180)
     out["rot_out3_90"] = data.rotate_data(x3, 90)
     preds = rng.uniform(-1, 1, size=(4 * 5, 51))
+    # appended after the draws above so the earlier vectors keep their values
+    rng2 = np.random.default_rng(11)
+    t2 = rng2.uniform(-1, 1, size=(6, 34))
+    t3 = rng2.uniform(-1, 1, size=(6, 51))
+    out["trans_in2"], out["trans_out2"] = t2, data.translation_data(t2, 0.07)
+    out["trans_in3"], out["trans_out3"] = t3, data.translation_data(t3, -0.03)
+    out["rot_out2_37"] = data.rotate_data(t2, 37.0)
     out["undo_in"] = preds
     out["undo_out_fr"] = data.undo(preds[:15], {"f": 1, "r": 2}, number_actions=2)
     out["undo_out_frt"] = data.undo(preds, {"f": 1, "r": 2, "t": 3}, number_actions=3,

@@ -634,6 +634,16 @@ def rotate_data(data: np.ndarray, angle: float = 180) -> np.ndarray:
     return r.reshape(data.shape).astype(data.dtype)
 
 
+def translation_data(data: np.ndarray, translation_factor: float = 0.5) -> np.ndarray:
+    """tools/data.py:27-54 (scalar factor): x, y (and a third channel) + t."""
+    t = data.copy().reshape((len(data), J, -1))
+    t[:, :, 0] += translation_factor
+    t[:, :, 1] += translation_factor
+    if t.shape[2] == 3:
+        t[:, :, 2] += translation_factor
+    return t.reshape(data.shape)
+
+
 def undo(preds: np.ndarray, op_ord: dict, number_actions: int, angle: float = 180,
          translation: float = 0.5) -> np.ndarray:
     """tools/data.py:269-287 (unflip :236-249, rotate, untranslate :205-218)."""

@@ -49,6 +49,9 @@ def test_tta_helpers_match_reference(golden_dir):
                                atol=1e-12)
     np.testing.assert_allclose(O.undo(g["undo_in"], {"f": 1, "r": 2, "t": 3}, 3, translation=0.05),
                                g["undo_out_frt"], atol=1e-12)
+    np.testing.assert_array_equal(O.translation_data(g["trans_in2"], 0.07), g["trans_out2"])
+    np.testing.assert_array_equal(O.translation_data(g["trans_in3"], -0.03), g["trans_out3"])
+    np.testing.assert_allclose(O.rotate_data(g["trans_in2"], 37.0), g["rot_out2_37"], atol=1e-12)
 
 
 def test_learning_rate_matches_notebook_logs(golden_dir):
