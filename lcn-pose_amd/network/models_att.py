@@ -185,13 +185,13 @@ class base_model(object):
                                                                  self.num_epochs))
                 print("  learning_rate = {:.2e}, loss_average = {:.4e}".format(learning_rate,
                                                                                loss_average))
-                training_error.append([time.time(), step, loss_average])
+                training_error.append([time.time(), step, float(loss_average)])
                 string, loss = self._evaluate_resident(val_data.shape[0], net)
                 losses.append(loss)
                 print("validation {}".format(string))
                 print("time: {:.0f}s (wall {:.0f}s)".format(time.process_time() - t_process,
                                                            time.time() - t_wall))
-                validation_error.append([0, step, loss])
+                validation_error.append([0, step, float(loss)])
                 self._write_summary(step, learning_rate, loss_average, loss)
                 ckpt.save(net, path, step, self._ckpt_meta())
                 if loss < min_loss:
@@ -228,8 +228,9 @@ class base_model(object):
         d = self._get_path("summaries")
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, "scalars.jsonl"), "a") as f:
-            f.write(json.dumps({"step": step, "learning_rate": lr, "loss/avg/total": loss_average,
-                                "validation/loss": val_loss}) + "\n")
+            f.write(json.dumps({"step": step, "learning_rate": float(lr),
+                                "loss/avg/total": float(loss_average),
+                                "validation/loss": float(val_loss)}) + "\n")
 
     def get_var(self, name):
         net = self._get_session()
