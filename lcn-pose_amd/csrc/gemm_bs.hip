@@ -24,8 +24,10 @@
 // coalesced 1 KB loads per input slab, prefetched one slab ahead in a second
 // register set); the weight block, shared by the 4 waves, goes into a double
 // LDS buffer by LDS-DMA, so there is one barrier per input slab.  The
-// accumulators start at bias + residual, and the BN-backward epilogue's z is
-// fetched at kernel start, so no epilogue operand load is exposed.  Measured
+// accumulators start at bias + residual; the BN-backward epilogue's z is
+// loaded after the loop, ahead of the output stores (prefetching it at kernel
+// start held 32 VGPRs through the loop and cost a wave per SIMD: 4 waves/SIMD
+// at <= 128 VGPRs is 3 % faster for the dX GEMM).  Measured
 // against a 128x64 LDS-staged tile with two barriers per slab: 124 vs 114
 // TFLOP/s at cfg3.
 //
@@ -95,7 +97,7 @@ namespace lcn {
   GSTEP(BUF, 6, P##6, CH) GSTEP(BUF, 7, P##7, CH) SCHED_SLAB
 
 template <int PRO, int EPI>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gemm_bs_kernel(GemmArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gemm_bs_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) float4 Wl[];  // [2][1024] (+ BN tables)
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int rtg = wg / a.n_out_slabs, so = wg - rtg * a.n_out_slabs;
@@ -148,9 +150,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   float4 zp0, zp1, zp2, zp3, zp4, zp5, zp6, zp7;
   float* ptab = (float*)(Wl + 2048);  // [4][64]: scale, shift, mean, rstd
   if constexpr (EPI == EPI_BNBACK) {
-    const float4* Z4 = (const float4*)a.epi_z + tbase;
-    zp0 = Z4[0]; zp1 = Z4[64]; zp2 = Z4[128]; zp3 = Z4[192];
-    zp4 = Z4[256]; zp5 = Z4[320]; zp6 = Z4[384]; zp7 = Z4[448];
     const int pk = threadIdx.x >> 6, ch = (so % (a.epi_F / kSlab)) * kSlab + lane;
     const float* src = pk == 0 ? a.epi_scale : pk == 1 ? a.epi_shift : pk == 2 ? a.epi_mean : a.epi_rstd;
     ptab[threadIdx.x] = src[ch];
@@ -184,6 +183,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   }
 
   // ---- epilogue ----
+  if constexpr (EPI == EPI_BNBACK) {
+    // z of the layer below, issued before the output stores so its latency
+    // overlaps them (keeping it live through the loop would cost 32 VGPRs,
+    // i.e. a wave per SIMD of occupancy)
+    const float4* Z4 = (const float4*)a.epi_z + tbase;
+    zp0 = Z4[0]; zp1 = Z4[64]; zp2 = Z4[128]; zp3 = Z4[192];
+    zp4 = Z4[256]; zp5 = Z4[320]; zp6 = Z4[384]; zp7 = Z4[448];
+  }
   float v[32];
 #pragma unroll
   for (int k = 0; k < 16; ++k) { v[k] = acc0[k]; v[16 + k] = acc1[k]; }
