@@ -166,6 +166,13 @@ int lcn_comm_unique_id(void* id_out /* 128 bytes */);
 int lcn_comm_init(void* handle, const void* id /* 128 bytes */, int32_t rank, int32_t world);
 int lcn_comm_allreduce_host(void* handle, double* values, int32_t count, int32_t op /* 0 sum, 1 max */);
 
+/* --- checkpoint I/O helpers (host only) -------------------------------- */
+/* CRC-32C of TensorFlow tensor-bundle checkpoints (tf.train.Saver files the
+ * reference writes and restores, models_att.py:256-260, 321-322, 457-461):
+ * leveldb/TF crc32c::Extend -- `crc` is the unmasked CRC of the preceding
+ * bytes (0 to start).  Used by lcn_amd/tf_bundle.py. */
+uint32_t lcn_crc32c(uint32_t crc, const void* data, int64_t n);
+
 /* --- instrumentation --------------------------------------------------- */
 /* kernel ids for lcn_kernel_timing */
 enum { LCN_K_GEMM_FWD = 0, LCN_K_GEMM_DX = 1, LCN_K_GEMM_DW = 2, LCN_K_NUM = 3 };

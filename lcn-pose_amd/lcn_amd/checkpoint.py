@@ -1,40 +1,109 @@
-"""Checkpoints in the reference's directory layout.
+"""Checkpoints in the reference's layout and TensorFlow's file format.
 
-tf.compat.v1.train.Saver(max_to_keep=1) writes ``<dir>/model-<step>.*`` plus a
-``checkpoint`` text file naming the latest prefix (models_att.py:161-162,
-256-260, 321-322); tf.train.latest_checkpoint reads that file (:457-459).
-This module keeps that layout; the payload is ``model-<step>.npz`` holding the
-flat parameters (TF variable order, lcn_param_layout), both Adam slots,
-global_step and the beta powers -- everything the reference checkpoint holds
-for this model.
+tf.compat.v1.train.Saver(max_to_keep=1) writes ``<dir>/model-<step>.index`` /
+``.data-00000-of-00001`` (+ ``.meta``) and a ``checkpoint`` text file naming
+the latest prefix (models_att.py:161-162, 256-260, 321-322);
+tf.train.latest_checkpoint reads that file and Saver.restore the bundle
+(:452-461).  ``save`` writes the same files through lcn_amd.tf_bundle under the
+variable names the reference graph gives its variables (``tf_name_map``):
+
+  mask                                         LC mask logits V (:557-566)
+  linear_model/{w1,b1,w4,b4}                   lift / output layer (:717-761)
+  linear_model/batch_normalization/{gamma,beta,moving_mean,moving_variance}
+  linear_model/two_linear_<i>/{w2_<i>,b2_<i>,w3_<i>,b3_<i>}      (:630-705)
+  linear_model/two_linear_<i>/batch_normalization{1,2}<i>/...    (:664-697)
+  <var>/Adam, <var>/Adam_1                     AdamOptimizer slots m, v
+  beta1_power, beta2_power, global_step        Adam / training state (:386-409)
+  loss/{mse_loss/Mean,add}/ExponentialMovingAverage[/biased,/local_step]
+                                               loss EMA(0.9) (:368-379)
+
+Keras BN moving statistics are written as their initial values (0, 1): the
+reference never runs their update ops (it trains and predicts with batch
+statistics, models_att.py:588-612).  These names follow TF1 / Keras naming
+rules; they are unverified against a real TF checkpoint (none exists offline,
+SURVEY §8f).  ``restore`` reads these files, and the earlier ``.npz`` payload.
 """
 from __future__ import annotations
 
 import glob
-import json
 import os
 import re
-from typing import Optional
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
+from . import tf_bundle
 
-def save(net, prefix: str, step: int, meta: Optional[dict] = None) -> str:
+
+def _bn_scope(name: str) -> Tuple[str, str]:
+    """our BN parameter name -> (TF layer scope, gamma|beta)."""
+    m = re.fullmatch(r"bn(\d+)_(gamma|beta)", name)
+    if not m:
+        raise KeyError(name)
+    tag, which = m.group(1), m.group(2)
+    if tag == "0":
+        return "linear_model/batch_normalization", which
+    kind, idx = tag[0], tag[1:]                      # "1<idx>" / "2<idx>"
+    return f"linear_model/two_linear_{idx}/batch_normalization{kind}{idx}", which
+
+
+def tf_name_map(layout) -> List[Tuple[str, str, int, tuple]]:
+    """(our name, TF variable name, offset, shape) per trainable variable."""
+    out = []
+    for name, off, shape in layout:
+        if name == "mask":
+            tf = "mask"
+        elif name in ("w1", "b1", "w4", "b4"):
+            tf = f"linear_model/{name}"
+        elif re.fullmatch(r"[wb][23]_\d+", name):
+            tf = f"linear_model/two_linear_{name.split('_')[1]}/{name}"
+        else:
+            scope, which = _bn_scope(name)
+            tf = f"{scope}/{which}"
+        out.append((name, tf, off, tuple(shape)))
+    return out
+
+
+def _ema_names(regularized: bool) -> Tuple[str, str]:
+    # loss() ops (:353-366): "loss/mse_loss/Mean" and the total "loss/add"
+    # ("loss/add_1" once the regularisation term is added)
+    return "loss/mse_loss/Mean", ("loss/add_1" if regularized else "loss/add")
+
+
+def to_tensors(net, loss_ema=None, regularized=False) -> Dict[str, np.ndarray]:
+    params = net.get_params()
+    m, v, gs, b1p, b2p = net.get_optimizer_state()
+    t: Dict[str, np.ndarray] = {}
+    for _, tf, off, shape in tf_name_map(net.param_layout()):
+        n = int(np.prod(shape))
+        t[tf] = params[off:off + n].reshape(shape).copy()
+        t[tf + "/Adam"] = m[off:off + n].reshape(shape).copy()
+        t[tf + "/Adam_1"] = v[off:off + n].reshape(shape).copy()
+        if tf.endswith("/gamma"):
+            scope = tf[:-len("/gamma")]
+            t[scope + "/moving_mean"] = np.zeros(shape, np.float32)
+            t[scope + "/moving_variance"] = np.ones(shape, np.float32)
+    t["beta1_power"] = np.float32(b1p).reshape(())
+    t["beta2_power"] = np.float32(b2p).reshape(())
+    t["global_step"] = np.int32(gs).reshape(())
+    biased, steps = loss_ema if loss_ema else (0.0, 0)
+    avg = biased / (1 - 0.9 ** steps) if steps else 0.0
+    for op in _ema_names(regularized):
+        base = op + "/ExponentialMovingAverage"
+        t[base] = np.float32(avg).reshape(())
+        t[base + "/biased"] = np.float32(biased).reshape(())
+        t[base + "/local_step"] = np.float32(steps).reshape(())
+    return t
+
+
+def save(net, prefix: str, step: int, meta: Optional[dict] = None, loss_ema=None) -> str:
+    """Saver.save(sess, prefix, global_step=step) with max_to_keep=1."""
     d = os.path.dirname(prefix)
     os.makedirs(d, exist_ok=True)
     base = os.path.basename(prefix)
-    params = net.get_params()
-    m, v, gs, b1p, b2p = net.get_optimizer_state()
-    layout = net.param_layout()
     out = f"{prefix}-{step}"
-    tmp = out + ".tmp.npz"
-    np.savez(tmp, params=params, adam_m=m, adam_v=v, global_step=np.int64(gs),
-             beta1_power=np.float32(b1p), beta2_power=np.float32(b2p),
-             names=np.array([n for n, _, _ in layout]),
-             offsets=np.array([o for _, o, _ in layout], np.int64),
-             meta=np.array(json.dumps(meta or {})))
-    os.replace(tmp, out + ".npz")
-    # max_to_keep=1
+    regularized = bool(meta and meta.get("regularization"))
+    tf_bundle.write_bundle(out, to_tensors(net, loss_ema, regularized))
     for old in glob.glob(os.path.join(d, base + "-*")):
         if not old.startswith(out + "."):
             os.remove(old)
@@ -45,24 +114,67 @@ def save(net, prefix: str, step: int, meta: Optional[dict] = None) -> str:
 
 
 def latest_checkpoint(directory: str) -> Optional[str]:
+    """tf.train.latest_checkpoint: the prefix the `checkpoint` file names
+    (absolute, or relative to the directory -- the reference's Kaggle files hold
+    absolute paths of another machine, README.md:84: fall back to the basename
+    in this directory then)."""
     f = os.path.join(directory, "checkpoint")
     if os.path.exists(f):
         m = re.search(r'model_checkpoint_path: "([^"]+)"', open(f).read())
         if m:
             p = m.group(1)
-            return p if os.path.isabs(p) else os.path.join(directory, p)
-    cands = sorted(glob.glob(os.path.join(directory, "model-*.npz")),
-                   key=lambda p: int(re.search(r"model-(\d+)", p).group(1)))
-    return cands[-1][:-4] if cands else None
+            p = p if os.path.isabs(p) else os.path.join(directory, p)
+            if _exists(p):
+                return p
+            local = os.path.join(directory, os.path.basename(p))
+            if _exists(local):
+                return local
+    cands = sorted({re.search(r"(model-\d+)", x).group(1)
+                    for x in glob.glob(os.path.join(directory, "model-*"))},
+                   key=lambda s: int(s.split("-")[1]))
+    return os.path.join(directory, cands[-1]) if cands else None
 
 
-def restore(net, prefix: str) -> None:
+def _exists(prefix: str) -> bool:
+    return os.path.exists(prefix + ".index") or os.path.exists(prefix + ".npz")
+
+
+def restore(net, prefix: str) -> Optional[Tuple[float, int]]:
+    """Saver.restore: parameters, Adam slots, beta powers, global_step.
+    Returns the loss EMA state (biased, steps) when the checkpoint has one."""
+    if prefix.endswith(".npz") or (not os.path.exists(prefix + ".index")
+                                   and os.path.exists(prefix + ".npz")):
+        return _restore_npz(net, prefix)
+    t = tf_bundle.read_bundle(prefix)
+    n = net.n_params
+    params, m, v = np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    for ours, tf, off, shape in tf_name_map(net.param_layout()):
+        if tf not in t:
+            raise ValueError(f"checkpoint {prefix} has no variable {tf} ({ours})")
+        if tuple(t[tf].shape) != shape:
+            raise ValueError(f"{tf}: checkpoint shape {t[tf].shape} != model shape {shape}")
+        k = int(np.prod(shape))
+        params[off:off + k] = t[tf].ravel()
+        if tf + "/Adam" in t:
+            m[off:off + k] = t[tf + "/Adam"].ravel()
+            v[off:off + k] = t[tf + "/Adam_1"].ravel()
+    net.set_params(params)
+    net.set_optimizer_state(m, v, int(t.get("global_step", 0)),
+                            float(t.get("beta1_power", 0.9)), float(t.get("beta2_power", 0.999)))
+    for op in ("loss/add", "loss/add_1"):  # the total loss's EMA
+        base = op + "/ExponentialMovingAverage"
+        if base + "/biased" in t:
+            return float(t[base + "/biased"]), int(t[base + "/local_step"])
+    return None
+
+
+def _restore_npz(net, prefix: str):
     path = prefix if prefix.endswith(".npz") else prefix + ".npz"
     with np.load(path, allow_pickle=False) as z:
         names = [str(s) for s in z["names"]]
-        layout = net.param_layout()
-        if names != [n for n, _, _ in layout]:
+        if names != [n for n, _, _ in net.param_layout()]:
             raise ValueError(f"checkpoint {path} does not match the model's variables")
         net.set_params(z["params"])
         net.set_optimizer_state(z["adam_m"], z["adam_v"], int(z["global_step"]),
                                 float(z["beta1_power"]), float(z["beta2_power"]))
+    return None

@@ -82,6 +82,7 @@ SIGNATURES = {
     "lcn_comm_unique_id": ([_vp], _i32),
     "lcn_comm_init": ([_vp, _vp, _i32, _i32], _i32),
     "lcn_comm_allreduce_host": ([_vp, _f64p, _i32, _i32], _i32),
+    "lcn_crc32c": ([ctypes.c_uint32, ctypes.c_char_p, _i64], ctypes.c_uint32),
     "lcn_set_timing": ([_vp, _i32], _i32),
     "lcn_kernel_timing": ([_vp, _i32, _i64p, _f64p, _f64p], _i32),
     "lcn_debug_tensor": ([_vp, _i32, _i32, _f32p, _i64], _i32),

@@ -9,8 +9,9 @@ gfx950) through lcn_amd.native; there is no CPU compute path.
 Deliberate differences from the reference, all documented in DESIGN.md:
   * resuming from a checkpoint restores the weights AND keeps them (the
     reference re-runs the initializer after restoring, :177-180);
-  * checkpoints are written by lcn_amd.checkpoint (params + Adam slots +
-    global_step + beta powers), not by tf.train.Saver.
+  * checkpoints are TensorFlow tensor bundles written without TensorFlow
+    (lcn_amd.checkpoint / tf_bundle: the .index / .data files and variable
+    names of tf.train.Saver, no .meta graph).
 """
 from __future__ import annotations
 
@@ -158,7 +159,9 @@ class base_model(object):
             starting_step = found
             print(f"Resuming from step {starting_step}")
             print(f"Restoring from checkpoint: {starting_checkpoint}")
-            ckpt.restore(net, ckpt.latest_checkpoint(starting_checkpoint))
+            ema = ckpt.restore(net, ckpt.latest_checkpoint(starting_checkpoint))
+            if ema is not None:
+                self._loss_ema = list(ema)
 
         losses = []
         # the deque of np.random.permutation() indices of :193-200, kept as an
@@ -193,10 +196,10 @@ class base_model(object):
                                                            time.time() - t_wall))
                 validation_error.append([0, step, float(loss)])
                 self._write_summary(step, learning_rate, loss_average, loss)
-                ckpt.save(net, path, step, self._ckpt_meta())
+                ckpt.save(net, path, step, self._ckpt_meta(), self._loss_ema)
                 if loss < min_loss:
                     min_loss = loss
-                    ckpt.save(net, best_path, step, self._ckpt_meta())
+                    ckpt.save(net, best_path, step, self._ckpt_meta(), self._loss_ema)
 
         print("validation loss: trough = {:.4f}, mean = {:.2f}".format(
             min_loss, np.mean(losses[-10:]) if losses else float("nan")))
@@ -324,4 +327,5 @@ class cgcnn(base_model):
     def _ckpt_meta(self):
         return {"F": self.F, "mask_type": self.mask_type, "num_layers": self.num_layers,
                 "in_F": self.in_F, "knn": self.knn, "residual": self.residual,
-                "batch_norm": self.batch_norm, "max_norm": self.max_norm}
+                "batch_norm": self.batch_norm, "max_norm": self.max_norm,
+                "regularization": self.regularization not in (0, None)}

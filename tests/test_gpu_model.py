@@ -68,7 +68,8 @@ def test_fit_predict_evaluate_checkpoints(model_dir, tmp_path):
     ck = model._get_path("checkpoints")
     for sub in ("final", "best"):
         assert os.path.exists(os.path.join(ck, sub, "checkpoint"))
-    assert os.path.exists(os.path.join(ck, "final", "model-10.npz"))
+    assert os.path.exists(os.path.join(ck, "final", "model-10.index"))
+    assert os.path.exists(os.path.join(ck, "final", "model-10.data-00000-of-00001"))
 
     # the batches are the reference deque's
     np.random.seed(5)
