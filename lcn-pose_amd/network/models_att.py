@@ -139,6 +139,9 @@ class base_model(object):
     def fit(self, train_data, train_labels, val_data, val_labels, output_dir=None,
             starting_checkpoint=None):
         """Training loop of models_att.py:148-286 (one lcn_train_step per step)."""
+        if self.dropout not in (0, None, 0.0):
+            # predict feeds dropout 0 (:102), so only training is affected
+            raise NotImplementedError("training with dropout > 0 is not implemented on the MI355X path yet")
         t_process, t_wall = time.process_time(), time.time()
         starting_step = 1
         net = self._net
@@ -290,8 +293,6 @@ class cgcnn(base_model):
         self.initialize_mask()
         if self.decay_type != "exp":
             raise AssertionError("not implemented lr decay types!")
-        if self.dropout not in (0, None, 0.0):
-            raise NotImplementedError("dropout > 0 is not implemented on the MI355X path yet")
         dp = self.decay_params or {"decay_steps": 32000, "decay_rate": 0.96}
         self._net = Network(F=self.F, in_F=in_F, num_layers=self.num_layers,
                             mask_type=self.mask_type, mask_matrix=self._mask_matrix,

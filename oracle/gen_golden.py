@@ -16,6 +16,9 @@ What it pins, and from where:
     - ``tools.data.flip_data / rotate_data / translation_data / undo`` on
       seeded inputs (data.py:10-25, 289-322, 27-54, 269-287), imported with an ``h5py``
       placeholder (data.py:3 imports it and never uses it).
+* ``ref_datareader.npz`` -- the reference's ``tools.data.DataReader``
+  (read_2d / read_3d / denormalize, data.py:338-489) on synthetic in-memory
+  items (``synthetic_gt``; float64 and float32 joints).
 * ``notebook_masks.npz`` -- the neighbour matrices printed by the reference's
   own Kaggle runs (parameter dumps in kaggle/custom-dataset-h36m.ipynb, knn=2,
   and kaggle/custom-dataset-humansc3d.ipynb, knn=1).
@@ -83,6 +86,43 @@ def ref_helpers():
     out["undo_out_fr"] = data.undo(preds[:15], {"f": 1, "r": 2}, number_actions=2)
     out["undo_out_frt"] = data.undo(preds, {"f": 1, "r": 2, "t": 3}, number_actions=3,
                                     translation=0.05)
+    return out
+
+
+def synthetic_gt(n, seed, dtype):
+    """In-memory dataset items with the reference's per-frame dict schema
+    (gendb*.py): joint_3d_image [17, 3] (pixels, depth), camera_param.name,
+    cameraid / videoid / subject / action."""
+    rng = np.random.default_rng(seed)
+    cams = ["54138969", "55011271", "58860488", "60457274", "cam_3", "17", "65906101"]
+    items = []
+    for i in range(n):
+        cam = cams[i % len(cams)]
+        j = np.concatenate([rng.uniform(0, 1000, (17, 2)), rng.uniform(-300, 300, (17, 1))], 1)
+        items.append({"joint_3d_image": j.astype(dtype), "camera_param": {"name": cam},
+                      "cameraid": cam, "videoid": i // 3, "subject": f"S{i % 3}",
+                      "action": f"a{i % 4}"})
+    return items
+
+
+def data_reader():
+    """tools.data.DataReader read_2d / read_3d / denormalize of the reference
+    on synthetic items (float64 and float32 joints)."""
+    _, _, data, _ = _import_reference()
+    out = {}
+    for tag, dt in (("f64", np.float64), ("f32", np.float32)):
+        tr, te = synthetic_gt(23, 1, dt), synthetic_gt(15, 2, dt)
+        r = data.DataReader()
+        x_tr, x_te = r.read_2d(tr, te)
+        y_tr, y_te = r.read_3d()
+        pred = np.random.default_rng(3).uniform(-1, 1, (15, 51))
+        res = r.denormalize(pred)
+        out[f"{tag}_x_train"], out[f"{tag}_x_test"] = x_tr, x_te
+        out[f"{tag}_y_train"], out[f"{tag}_y_test"] = y_tr, y_te
+        out[f"{tag}_pred"] = pred
+        out[f"{tag}_denorm"] = np.stack([d["result"] for d in res])
+        out[f"{tag}_denorm_keys"] = np.array([f"{d['cameraid']}|{d['videoid']}|{d['subject']}|{d['action']}"
+                                              for d in res])
     return out
 
 
@@ -165,6 +205,7 @@ def main():
     os.makedirs(OUT, exist_ok=True)
     np.savez(os.path.join(OUT, "ref_helpers.npz"), **ref_helpers())
     np.savez(os.path.join(OUT, "notebook_masks.npz"), **notebook_masks())
+    np.savez(os.path.join(OUT, "ref_datareader.npz"), **data_reader())
     with open(os.path.join(OUT, "notebook_facts.json"), "w") as f:
         json.dump(notebook_facts(), f, indent=1)
     for name, d in oracle_vectors().items():

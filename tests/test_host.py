@@ -56,3 +56,35 @@ def test_mean_batch_loss_is_float32_accumulation():
         ref += l
     ref = ref * 200 / 550
     assert got == ref and np.asarray(got).dtype == np.asarray(ref).dtype
+
+
+@pytest.mark.parametrize("tag,dt", [("f64", np.float64), ("f32", np.float32)])
+def test_datareader_matches_reference_bitwise(golden_dir, tag, dt):
+    """tools/data.py DataReader (read_2d / read_3d / denormalize) against the
+    reference's own class on the same items (oracle/gen_golden.py)."""
+    import gen_golden as G
+    from tools import data
+    g = np.load(os.path.join(golden_dir, "ref_datareader.npz"))
+    tr, te = G.synthetic_gt(23, 1, dt), G.synthetic_gt(15, 2, dt)
+    r = data.DataReader()
+    x_tr, x_te = r.read_2d(tr, te)
+    y_tr, y_te = r.read_3d()
+    for name, got in (("x_train", x_tr), ("x_test", x_te), ("y_train", y_tr), ("y_test", y_te)):
+        np.testing.assert_array_equal(got, g[f"{tag}_{name}"], err_msg=name)
+    res = r.denormalize(g[f"{tag}_pred"])
+    np.testing.assert_array_equal(np.stack([d["result"] for d in res]), g[f"{tag}_denorm"])
+    keys = [f"{d['cameraid']}|{d['videoid']}|{d['subject']}|{d['action']}" for d in res]
+    assert keys == list(g[f"{tag}_denorm_keys"])
+
+
+def test_augmentation_helpers_match_reference(golden_dir):
+    from tools import data
+    g = np.load(os.path.join(golden_dir, "ref_helpers.npz"))
+    np.testing.assert_array_equal(data.flip_data(g["flip_in2"]), g["flip_out2"])
+    np.testing.assert_array_equal(data.flip_data(g["flip_in3"]), g["flip_out3"])
+    np.testing.assert_array_equal(data.translation_data(g["trans_in2"], 0.07), g["trans_out2"])
+    np.testing.assert_array_equal(data.translation_data(g["trans_in3"], -0.03), g["trans_out3"])
+    np.testing.assert_allclose(data.rotate_data(g["rot_in2"], 180), g["rot_out2"], atol=1e-12)
+    np.testing.assert_allclose(data.rotate_data(g["rot_in3"], 90), g["rot_out3_90"], atol=1e-12)
+    np.testing.assert_allclose(data.undo(g["undo_in"], {"f": 1, "r": 2, "t": 3}, 3, translation=0.05),
+                               g["undo_out_frt"], atol=1e-12)
