@@ -166,6 +166,22 @@ int lcn_comm_unique_id(void* id_out /* 128 bytes */);
 int lcn_comm_init(void* handle, const void* id /* 128 bytes */, int32_t rank, int32_t world);
 int lcn_comm_allreduce_host(void* handle, double* values, int32_t count, int32_t op /* 0 sum, 1 max */);
 
+/* --- evaluation -------------------------------------- */
+/* evaluate.py's per-frame loop (evaluate.py:53-73) in one launch, float64:
+ * every frame's prediction goes from the image frame to the camera frame
+ * (tools/tools.py:183-194: box width / 2000 depth ratio, root depth, pinhole
+ * cx, cy, fx, fy), is Procrustes-aligned to the ground truth when protocol2
+ * != 0 (align_to_gt = procrustes(gt, pred)[1], tools.py:96-202), and
+ * err[f][j] = |pred_j - gt_j| (evaluate.py:61).
+ *   pred [n][17][3] image-frame predictions (inference.py's result rows)
+ *   gt   [n][17][3] joint_3d_camera        box [n][4] (x0, y0, x1, y1)
+ *   cam  [n][4] (cx, cy, fx, fy)           root_depth [n]
+ * Host arrays in, host err [n][17] out; no handle (errors: lcn_last_error(NULL)).
+ * Protocol 1 is bit-identical to the reference's numpy; protocol 2 agrees to
+ * rounding (a Jacobi SVD instead of LAPACK's). */
+int lcn_eval_mpjpe(int32_t device, int64_t n, const double* pred, const double* gt, const double* box,
+                   const double* cam, const double* root_depth, int32_t protocol2, double* err);
+
 /* --- checkpoint I/O helpers (host only) -------------------------------- */
 /* CRC-32C of TensorFlow tensor-bundle checkpoints (tf.train.Saver files the
  * reference writes and restores, models_att.py:256-260, 321-322, 457-461):

@@ -1362,3 +1362,55 @@ int lcn_debug_tensor(void* handle, int32_t kind, int32_t idx, float* host, int64
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// evaluate.py's per-frame error loop (evaluate.py:53-73) as one launch:
+// image_to_camera_frame (tools.py:183-194), optional Procrustes alignment
+// (tools.py:96-202), per-joint Euclidean error.  Handle-free: it needs no
+// network; errors are reported through lcn_last_error(NULL).
+extern "C" int lcn_eval_mpjpe(int32_t device, int64_t n, const double* pred, const double* gt,
+                              const double* box, const double* cam, const double* root_depth,
+                              int32_t protocol2, double* err) {
+  g_create_error.clear();
+  if (n < 0 || (n > 0 && (!pred || !gt || !box || !cam || !root_depth || !err))) {
+    g_create_error = "lcn_eval_mpjpe: null argument or negative frame count";
+    return LCN_E_ARG;
+  }
+  if (n == 0) return LCN_OK;
+  struct Guard {
+    hipStream_t s = nullptr;
+    double* d[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    ~Guard() {
+      if (s) hipStreamSynchronize(s);
+      for (double* p : d)
+        if (p) hipFree(p);
+      if (s) hipStreamDestroy(s);
+    }
+  } g;
+  auto fail = [](const char* what, hipError_t e) {
+    g_create_error = std::string("lcn_eval_mpjpe: ") + what + ": " + hipGetErrorString(e);
+    return LCN_E_HIP;
+  };
+  hipError_t e;
+  if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
+  if ((e = hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
+  const size_t sz[6] = {(size_t)n * 51, (size_t)n * 51, (size_t)n * 4, (size_t)n * 4, (size_t)n,
+                        (size_t)n * kJ};
+  const double* src[5] = {pred, gt, box, cam, root_depth};
+  for (int i = 0; i < 6; ++i) {
+    if (hipMalloc(&g.d[i], sz[i] * sizeof(double)) != hipSuccess) {
+      g.d[i] = nullptr;
+      g_create_error = "lcn_eval_mpjpe: hipMalloc (" + std::to_string(sz[i] * 8) + " bytes)";
+      return LCN_E_NOMEM;
+    }
+    if (i < 5 && (e = hipMemcpyAsync(g.d[i], src[i], sz[i] * sizeof(double), hipMemcpyHostToDevice, g.s)) !=
+                     hipSuccess)
+      return fail("copy in", e);
+  }
+  launch_mpjpe(n, g.d[0], g.d[1], g.d[2], g.d[3], g.d[4], protocol2 ? 1 : 0, g.d[5], g.s);
+  if ((e = hipGetLastError()) != hipSuccess) return fail("launch", e);
+  if ((e = hipMemcpyAsync(err, g.d[5], sz[5] * sizeof(double), hipMemcpyDeviceToHost, g.s)) != hipSuccess)
+    return fail("copy out", e);
+  if ((e = hipStreamSynchronize(g.s)) != hipSuccess) return fail("synchronize", e);
+  return LCN_OK;
+}

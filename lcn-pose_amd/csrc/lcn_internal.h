@@ -148,6 +148,10 @@ void launch_gather_rows(const void* ds, int dtype, int64_t rows, int cols, const
 void launch_store_pred(const float* out, int64_t n, double* pred, hipStream_t s);
 void launch_tta_undo(const double* pred, int64_t N, const Augment& undo, double* out, hipStream_t s);
 void launch_batch_loss(const double* loss_sum, double count, float* losses, int i, hipStream_t s);
+// evaluate.py per-frame, per-joint error (kernels_eval.hip): pred / gt [n][17][3],
+// box [n][4], cam [n][4] = (cx, cy, fx, fy), root_depth [n] -> err [n][17]
+void launch_mpjpe(int64_t n, const double* pred, const double* gt, const double* box, const double* cam,
+                  const double* root_depth, int protocol2, double* err, hipStream_t s);
 
 // ----------------------------------------------------------------------------
 // BatchNorm (batch statistics), activation, BN backward

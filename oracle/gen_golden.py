@@ -19,6 +19,9 @@ What it pins, and from where:
 * ``ref_datareader.npz`` -- the reference's ``tools.data.DataReader``
   (read_2d / read_3d / denormalize, data.py:338-489) on synthetic in-memory
   items (``synthetic_gt``; float64 and float32 joints).
+* ``ref_eval.npz`` -- evaluate.py's per-frame errors (protocol 1 and 2) from
+  the reference's ``tools.tools.image_to_camera_frame`` / ``align_to_gt``
+  (tools.py:96-202) on synthetic frames (``synthetic_frames``).
 * ``notebook_masks.npz`` -- the neighbour matrices printed by the reference's
   own Kaggle runs (parameter dumps in kaggle/custom-dataset-h36m.ipynb, knn=2,
   and kaggle/custom-dataset-humansc3d.ipynb, knn=1).
@@ -126,6 +129,63 @@ def data_reader():
     return out
 
 
+def synthetic_frames(n, seed):
+    """Camera-space ground truth and image-frame predictions with the schema
+    evaluate.py reads (joint_3d_camera, box, camera_param cx/cy/fx/fy,
+    root_depth): predictions are the ground truth projected the way
+    image_to_camera_frame inverts it, then rotated, scaled and perturbed."""
+    rng = np.random.default_rng(seed)
+    root = np.stack([rng.uniform(-500, 500, n), rng.uniform(-300, 300, n), rng.uniform(3500, 6500, n)], 1)
+    gt = root[:, None, :] + rng.uniform(-800, 800, (n, 17, 3))
+    gt[:, 0] = root
+    box = np.stack([rng.uniform(0, 400, n), rng.uniform(0, 400, n)], 1)
+    box = np.concatenate([box, box + rng.uniform(200, 900, (n, 1))], 1)
+    cam = np.stack([rng.uniform(480, 520, n), rng.uniform(480, 520, n),
+                    rng.uniform(1100, 1200, n), rng.uniform(1100, 1200, n)], 1)
+    ang = rng.uniform(-0.3, 0.3, n)
+    c, s_ = np.cos(ang), np.sin(ang)
+    pert = gt.copy()
+    x0 = pert[..., 0] - root[:, None, 0]
+    z0 = pert[..., 2] - root[:, None, 2]
+    pert[..., 0] = root[:, None, 0] + c[:, None] * x0 - s_[:, None] * z0
+    pert[..., 2] = root[:, None, 2] + s_[:, None] * x0 + c[:, None] * z0
+    pert = root[:, None, :] + (pert - root[:, None, :]) * rng.uniform(0.9, 1.1, (n, 1, 1))
+    pert += rng.normal(0, 20, pert.shape)
+    ratio = (box[:, 2] - box[:, 0] + 1) / 2000.0
+    pred = np.empty_like(pert)
+    pred[..., 0] = pert[..., 0] / pert[..., 2] * cam[:, None, 2] + cam[:, None, 0]
+    pred[..., 1] = pert[..., 1] / pert[..., 2] * cam[:, None, 3] + cam[:, None, 1]
+    pred[..., 2] = (pert[..., 2] - root[:, None, 2]) * ratio[:, None]
+    return pred, gt, box, cam, root[:, 2].copy()
+
+
+def ref_eval():
+    """Per-frame evaluation of the reference (evaluate.py:53-61) with its own
+    tools.tools.image_to_camera_frame / align_to_gt (tools.py:96-202) on
+    synthetic frames; matplotlib is imported by tools.py for plotting only."""
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, os.path.join(REF, "tools"))
+    import tools as ref_tools  # noqa
+    pred, gt, box, cam, rd = synthetic_frames(257, seed=21)
+    out = {"pred": pred, "gt": gt, "box": box, "cam": cam, "root_depth": rd}
+    for proto in (1, 2):
+        err = np.empty((len(pred), 17))
+        cam_pose = np.empty_like(pred)
+        for i in range(len(pred)):
+            camera = {"cx": cam[i, 0], "cy": cam[i, 1], "fx": cam[i, 2], "fy": cam[i, 3]}
+            p = ref_tools.image_to_camera_frame(pose3d_image_frame=pred[i], box=box[i], camera=camera,
+                                                rootIdx=0, root_depth=rd[i])
+            if proto == 1:
+                cam_pose[i] = p
+            else:
+                p = ref_tools.align_to_gt(pose=p, pose_gt=gt[i])
+                cam_pose[i] = p
+            err[i] = np.sqrt(np.square(p - gt[i]).sum(axis=1))
+        out[f"p{proto}_pose"] = cam_pose
+        out[f"p{proto}_err"] = err
+    return out
+
+
 def notebook_masks():
     res = {}
     for fname, key in (("custom-dataset-h36m.ipynb", "nb_h36m_knn2"),
@@ -206,6 +266,7 @@ def main():
     np.savez(os.path.join(OUT, "ref_helpers.npz"), **ref_helpers())
     np.savez(os.path.join(OUT, "notebook_masks.npz"), **notebook_masks())
     np.savez(os.path.join(OUT, "ref_datareader.npz"), **data_reader())
+    np.savez_compressed(os.path.join(OUT, "ref_eval.npz"), **ref_eval())
     with open(os.path.join(OUT, "notebook_facts.json"), "w") as f:
         json.dump(notebook_facts(), f, indent=1)
     for name, d in oracle_vectors().items():

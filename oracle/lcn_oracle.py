@@ -321,10 +321,15 @@ def reg_loss(cfg: Config, params, dtype=np.float64) -> float:
 # Backward (analytic)
 # ----------------------------------------------------------------------------
 
-def _bn_act_backward(cfg, dh, rec, F, gamma):
+def _bn_act_backward(cfg, dh, rec, F, gamma, pos=None):
+    """``pos`` (test hook): the LeakyReLU branch mask u > 0 to use instead of
+    this pass's own -- a float32 forward whose u lands on the other side of 0
+    than the float64 one takes the other branch of the kink."""
     B = dh.shape[0]
     u = rec["u"]
-    du = dh * np.where(u > 0, dh.dtype.type(1), dh.dtype.type(cfg.leaky_alpha))
+    if pos is None:
+        pos = u > 0
+    du = dh * np.where(pos, dh.dtype.type(1), dh.dtype.type(cfg.leaky_alpha))
     st = rec["st"]
     if st is None:
         return du, None, None
@@ -339,11 +344,15 @@ def _bn_act_backward(cfg, dh, rec, F, gamma):
 
 
 def backward(cfg: Config, params, cache, lab: np.ndarray, dtype=np.float32,
-             global_batch: Optional[int] = None) -> Dict[str, np.ndarray]:
+             global_batch: Optional[int] = None,
+             kinks: Optional[Dict[int, np.ndarray]] = None) -> Dict[str, np.ndarray]:
     """Gradients of the MSE loss (+ regularisation) w.r.t. every trainable.
 
     ``global_batch`` lets a shard scale its loss gradient by the global batch
-    (data-parallel decomposition tests)."""
+    (data-parallel decomposition tests).  ``kinks`` maps a linear layer index
+    to the [B, H] mask u > 0 to differentiate LeakyReLU with (tests compare a
+    float32 device run against float64 at the device's own kink branches)."""
+    kinks = kinks or {}
     P = {k: np.asarray(v, dtype) for k, v in params.items()}
     layers = layer_names(cfg)
     eff = cache["eff"]
@@ -372,7 +381,7 @@ def backward(cfg: Config, params, cache, lab: np.ndarray, dtype=np.float32,
             wn, bname, bnp, fin, fout = layers[k]
             rec = recs[k]
             gamma = P[bnp + "_gamma"] if bnp else None
-            dz, dgam, dbet = _bn_act_backward(cfg, dh, rec, fout, gamma)
+            dz, dgam, dbet = _bn_act_backward(cfg, dh, rec, fout, gamma, kinks.get(k))
             if bnp:
                 g[bnp + "_gamma"], g[bnp + "_beta"] = dgam, dbet
             dWe[wn] = rec["a"].T @ dz
@@ -384,7 +393,7 @@ def backward(cfg: Config, params, cache, lab: np.ndarray, dtype=np.float32,
     wn, bname, bnp, fin, fout = layers[0]
     rec = recs[0]
     gamma = P[bnp + "_gamma"] if bnp else None
-    dz, dgam, dbet = _bn_act_backward(cfg, dh, rec, fout, gamma)
+    dz, dgam, dbet = _bn_act_backward(cfg, dh, rec, fout, gamma, kinks.get(0))
     if bnp:
         g[bnp + "_gamma"], g[bnp + "_beta"] = dgam, dbet
     dWe[wn] = rec["a"].T @ dz
