@@ -109,6 +109,12 @@ int lcn_forward_loss(void* handle, const float* x, const float* labels, float* o
 int lcn_train_step(void* handle, const float* x, const float* labels, int64_t batch,
                    int32_t flags, float* loss_out, float* lr_out);
 int lcn_synchronize(void* handle);
+/* tf.nn.dropout(rate) after every BN + LeakyReLU in training steps
+ * (models_att.py:673, 700, 742; predict runs without it, :102).  rate in
+ * [0, 1), 0 = off.  The masks are a counter-based hash of (seed, training-step
+ * number since this call, layer, global row, column) -- see lcn_internal.h
+ * Dropout; TF's own random stream cannot be reproduced. */
+int lcn_set_dropout(void* handle, float rate, uint64_t seed);
 
 /* --- device-resident data (on-device datasets; no host copies per step) */
 int lcn_device_buffer(void* handle, int32_t slot, int64_t bytes, void** dptr);

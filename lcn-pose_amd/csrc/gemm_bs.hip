@@ -263,6 +263,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   }
   // EPI_BNBACK: du = dh * leaky'(u(z)), zhat = (z - mean) * rstd of the layer
   // below; pass 0 reduces du, pass 1 du * zhat
+  // dropout of the layer below (tf.nn.dropout's gradient: dh * mask * scale),
+  // applied to the partials only -- the stored dh stays the incoming gradient
+  if (a.epi_drop.rate > 0.f) {
+    const int64_t row = (int64_t)rt * kRT + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = drop_apply(a.epi_drop, row, so * kSlab + acc_feature(i, h), v[i]);
+  }
 #define BNBACK_EPI(P)                                                                      \
   {                                                                                        \
     const float4 zq[8] = {P##0, P##1, P##2, P##3, P##4, P##5, P##6, P##7};                 \

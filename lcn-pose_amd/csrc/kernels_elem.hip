@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const float4* __restrict__ 
                                                      float4* __restrict__ h,
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int F, int S,
-                                                     float alpha, int64_t n4) {
+                                                     float alpha, int64_t n4, Dropout drop) {
   const int spj = F / 64;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     const int c4 = (int)(i & 511);
@@ -198,6 +198,14 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const float4* __restrict__ 
     v.y = leaky(fmaf(v.y, sc.y, sh.y), alpha);
     v.z = leaky(fmaf(v.z, sc.z, sh.z), alpha);
     v.w = leaky(fmaf(v.w, sc.w, sh.w), alpha);
+    if (drop.rate > 0.f) {  // row / column of this float4 in the row-tile layout
+      const int64_t row = (i >> 9) / S * kRT + (c4 & 31);
+      const int col = (int)((i >> 9) % S) * 64 + 8 * (c4 >> 6) + 4 * ((c4 >> 5) & 1);
+      v.x = drop_apply(drop, row, col, v.x);
+      v.y = drop_apply(drop, row, col + 1, v.y);
+      v.z = drop_apply(drop, row, col + 2, v.z);
+      v.w = drop_apply(drop, row, col + 3, v.w);
+    }
     if (res) {
       const float4 r = res[i];
       v.x = r.x + v.x; v.y = r.y + v.y; v.z = r.z + v.z; v.w = r.w + v.w;
@@ -207,11 +215,12 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const float4* __restrict__ 
 }
 
 void launch_bn_act(const float* z, const float* res, float* h, const float* scale,
-                   const float* shift, int F, float alpha, int B, int S, hipStream_t s) {
+                   const float* shift, int F, float alpha, int B, int S, const Dropout& drop,
+                   hipStream_t s) {
   const int64_t n4 = tiled_floats(B, S) / 4;
   const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 256 * 16);
   hipLaunchKernelGGL(bn_act_kernel, dim3(grid), dim3(256), 0, s, (const float4*)z,
-                     (const float4*)res, (float4*)h, scale, shift, F, S, alpha, n4);
+                     (const float4*)res, (float4*)h, scale, shift, F, S, alpha, n4, drop);
 }
 
 // per-kEwRows-row column sums of a 1-slab row-tiled src (the output bias

@@ -112,6 +112,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
         c.c3 = *(const float4*)(tab + 512 + f);
         return c;
       };
+      if (a.d_drop.rate > 0.f) {  // tf.nn.dropout's gradient: dh * mask * scale
+        const int64_t row = base + lr;
+        const int col = so * kSlab + f0;
+        rd0.x = drop_apply(a.d_drop, row, col, rd0.x);
+        rd0.y = drop_apply(a.d_drop, row, col + 1, rd0.y);
+        rd0.z = drop_apply(a.d_drop, row, col + 2, rd0.z);
+        rd0.w = drop_apply(a.d_drop, row, col + 3, rd0.w);
+        rd1.x = drop_apply(a.d_drop, row, col + 32, rd1.x);
+        rd1.y = drop_apply(a.d_drop, row, col + 33, rd1.y);
+        rd1.z = drop_apply(a.d_drop, row, col + 34, rd1.z);
+        rd1.w = drop_apply(a.d_drop, row, col + 35, rd1.w);
+      }
       rd0 = bnback4(rd0, rz0, coef(f0), a.alpha);
       rd1 = bnback4(rd1, rz1, coef(f0 + 32), a.alpha);
       if (writer && v) {

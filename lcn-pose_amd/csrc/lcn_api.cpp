@@ -86,6 +86,15 @@ struct Handle {
   float *x = nullptr, *lab = nullptr, *out = nullptr, *dy = nullptr, *yout = nullptr;
   float* xin = nullptr;           // host-staged row-major input [Bmax][17*in_F]
   std::vector<float*> Z, Hb;
+  // dropout (lcn_set_dropout): rate, TF's scale 1/(1-rate), seed, train-step
+  // counter; drop_on while a training step runs; Gb = the dropped inner
+  // activation g of each block (materialised only with dropout, for the
+  // second GEMM of the block and its weight gradient)
+  float drop_rate = 0.f, drop_scale = 1.f;
+  uint32_t drop_seed = 0, step_seed = 0;
+  uint64_t drop_calls = 0;
+  bool drop_on = false;
+  std::vector<float*> Gb;
   // DH: gradient w.r.t. a block output h_l; DG: w.r.t. the inner activation g;
   // DZ: dz of a hidden layer, stored by its weight-gradient GEMM
   float *DH = nullptr, *DG = nullptr, *DZ = nullptr;
@@ -488,6 +497,20 @@ void tstop(Handle* h, int k, hipEvent_t* pair, double flops) {
   h->timers[k].flops += flops;
 }
 
+// the dropout of BN layer k in the running training step (rate 0 = none)
+Dropout drop_of(const Handle* h, int k, int64_t B) {
+  Dropout d{};
+  d.rate = 0.f;
+  d.scale = 1.f;
+  if (!h->drop_on) return d;
+  d.rate = h->drop_rate;
+  d.scale = h->drop_scale;
+  d.lseed = fmix32(h->step_seed ^ ((uint32_t)(k + 1) * 0x9e3779b9u));
+  d.H = h->H;
+  d.row0 = (int64_t)h->rank * B;
+  return d;
+}
+
 int prep_weights(Handle* h) {
   hipStream_t s = h->stream;
   launch_mask(h->learnable ? h->theta + h->mask_off : nullptr, h->Cd, h->learnable, h->Md, h->Sd, s);
@@ -574,6 +597,7 @@ int gemm(Handle* h, const GemmCall& c, int B) {
     a.epi_shift = st.shift;
     a.epi_mean = st.mean;
     a.epi_rstd = st.rstd;
+    a.epi_drop = drop_of(h, c.epi_layer, B);
   }
   a.epi_F = h->F;
   a.B = B;
@@ -622,6 +646,7 @@ int gemm_dw(Handle* h, const Operand& A, const Operand& D, const int2* blk, int 
     a.d_c123 = h->batch_norm ? h->c123 : h->ident_c123;
     a.d_F = h->F;
     a.dz_out = dz_out;
+    a.d_drop = drop_of(h, D.layer, B);
   }
   a.spj_a = h->spj;
   a.spj_d = h->spj;
@@ -675,6 +700,8 @@ int bn_back(Handle* h, int k, int B) {
 int forward(Handle* h, int B, bool with_labels, bool train) {
   hipStream_t s = h->stream;
   const int S = h->nslab, nl = h->nl;
+  // tf.nn.dropout runs in training steps only (predict feeds rate 0, :102)
+  h->drop_on = train && h->drop_rate > 0.f;
   CHECK(prep_weights(h));
   const int epi = h->batch_norm ? EPI_BNFWD : EPI_NONE;
   // lift z0 = x . W1e + b1 (models_att.py:714-729): x padded to one 64-wide slab
@@ -682,17 +709,25 @@ int forward(Handle* h, int B, bool with_labels, bool train) {
   CHECK(gemm(h, GemmCall{raw(h->x, 1), h->wl[0].blk_fwd, h->thin_ptr, h->thin_idx, S,
                          h->theta + h->b_off[0], h->Z[0], S, nullptr, epi, -1, -1, thin_flops}, B));
   CHECK(bn_stats(h, 0, B));
-  launch_bn_act(h->Z[0], nullptr, h->Hb[0], h->bn[0].scale, h->bn[0].shift, h->F, h->alpha, B, S, s);
+  launch_bn_act(h->Z[0], nullptr, h->Hb[0], h->bn[0].scale, h->bn[0].shift, h->F, h->alpha, B, S,
+                drop_of(h, 0, B), s);
   // two_linear blocks (models_att.py:630-705)
   for (int l = 0; l < h->L; ++l) {
     const int k1 = 2 * l + 1, k2 = 2 * l + 2;
     CHECK(gemm_hidden(h, k1, LCN_K_GEMM_FWD, raw(h->Hb[l], S), h->Z[k1], nullptr, epi, -1, B));
     CHECK(bn_stats(h, k1, B));
-    CHECK(gemm_hidden(h, k2, LCN_K_GEMM_FWD, Operand{h->Z[k1], S, PRO_BNACT, k1}, h->Z[k2],
-                      nullptr, epi, -1, B));
+    // g = dropout(leaky(BN(z1))): fused into the next GEMM's operand load, or
+    // materialised when dropout is on (the mask is per element, not per slab)
+    Operand g{h->Z[k1], S, PRO_BNACT, k1};
+    if (h->drop_on) {
+      launch_bn_act(h->Z[k1], nullptr, h->Gb[l], h->bn[k1].scale, h->bn[k1].shift, h->F, h->alpha, B, S,
+                    drop_of(h, k1, B), s);
+      g = raw(h->Gb[l], S);
+    }
+    CHECK(gemm_hidden(h, k2, LCN_K_GEMM_FWD, g, h->Z[k2], nullptr, epi, -1, B));
     CHECK(bn_stats(h, k2, B));
     launch_bn_act(h->Z[k2], h->residual ? h->Hb[l] : nullptr, h->Hb[l + 1], h->bn[k2].scale,
-                  h->bn[k2].shift, h->F, h->alpha, B, S, s);
+                  h->bn[k2].shift, h->F, h->alpha, B, S, drop_of(h, k2, B), s);
   }
   // output layer y = h_L . W4e + b4 into a 1-slab buffer (51 used), then the
   // output assembly, loss and d out (models_att.py:749-773, :356)
@@ -740,7 +775,8 @@ int backward(Handle* h, int B) {
     const int below = l > 0 ? k1 - 1 : 0;  // BN layer under block l's input h_l
     // DH = dh_{l+1}: gradient of the block output
     CHECK(bn_back(h, k2, B));
-    CHECK(gemm_dw(h, Operand{h->Z[k1], S, PRO_BNACT, k1}, Operand{h->DH, S, PRO_BNBACK, k2},
+    const Operand g = h->drop_on ? raw(h->Gb[l], S) : Operand{h->Z[k1], S, PRO_BNACT, k1};
+    CHECK(gemm_dw(h, g, Operand{h->DH, S, PRO_BNBACK, k2},
                   h->blk, h->nblk, h->rg + h->wl[k2].w_off, H, H, H, B, true,
                   h->DZ));                                             // dW_k2 = g^T dz2; DZ = dz2
     CHECK(gemm_hidden(h, k2, LCN_K_GEMM_DX, raw(h->DZ, S), h->DG, nullptr, EPI_BNBACK, k1, B));
@@ -1005,6 +1041,9 @@ int lcn_forward_loss(void* handle, const float* x, const float* labels, float* o
 
 static int run_train_step(Handle* h, int64_t B, int32_t flags, float* loss_out, float* lr_out) {
   const float lr = h->lr0 * powf(h->decay_rate, (float)h->global_step / (float)h->decay_steps);
+  // dropout masks of this step: seed of training step number drop_calls
+  h->step_seed = fmix32(h->drop_seed + fmix32((uint32_t)h->drop_calls + 0x9e3779b9u));
+  if (h->drop_rate > 0.f) h->drop_calls++;
   CHECK(forward(h, (int)B, true, true));
   if (h->world > 1) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
   CHECK(backward(h, (int)B));
@@ -1412,5 +1451,25 @@ extern "C" int lcn_eval_mpjpe(int32_t device, int64_t n, const double* pred, con
   if ((e = hipMemcpyAsync(err, g.d[5], sz[5] * sizeof(double), hipMemcpyDeviceToHost, g.s)) != hipSuccess)
     return fail("copy out", e);
   if ((e = hipStreamSynchronize(g.s)) != hipSuccess) return fail("synchronize", e);
+  return LCN_OK;
+}
+
+// tf.nn.dropout(rate) after every BN + LeakyReLU of the training step
+// (models_att.py:673, 700, 742); masks from (seed, training-step counter),
+// see lcn_internal.h Dropout.  rate 0 switches it off.
+extern "C" int lcn_set_dropout(void* handle, float rate, uint64_t seed) {
+  Handle* h = (Handle*)handle;
+  if (!h) return LCN_E_ARG;
+  if (!(rate >= 0.f && rate < 1.f)) { h->err = "dropout rate must be in [0, 1)"; return LCN_E_ARG; }
+  HIPC(hipSetDevice(h->device));
+  HIPC(hipStreamSynchronize(h->stream));
+  if (rate > 0.f && h->Gb.empty()) {
+    h->Gb.assign(h->L, nullptr);
+    for (auto& g : h->Gb) CHECK(dalloc(h, &g, (size_t)tiled_floats(h->Bmax, h->nslab)));
+  }
+  h->drop_rate = rate;
+  h->drop_scale = 1.f / (1.f - rate);  // TF: scale = 1 / (1 - rate) in float32
+  h->drop_seed = (uint32_t)seed ^ (uint32_t)(seed >> 32);
+  h->drop_calls = 0;
   return LCN_OK;
 }

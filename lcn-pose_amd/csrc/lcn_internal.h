@@ -43,6 +43,38 @@ __host__ __device__ inline int frag_ix(int n, int k) {
 }
 
 // ----------------------------------------------------------------------------
+// Dropout, tf.nn.dropout(y, rate) after every BN + LeakyReLU of the training
+// graph (models_att.py:673, 700, 742).  The mask is counter based, so the
+// backward regenerates it instead of storing it: element (row b, column c) of
+// BN layer k in one training step is kept iff
+//   ((fmix32(fmix32(lo ^ lseed) + hi) >> 8) * 2^-24) >= rate,
+// key = (row0 + b) * H + c = hi:lo, lseed = fmix32(step_seed ^ (k+1)*0x9e3779b9)
+// (set by the host per step and layer); a kept value is x * scale with
+// scale = float(1 / (1 - rate)), as TF's dropout computes it, a dropped one 0.
+// oracle/lcn_oracle.py restates the same function (dropout_mask).
+// ----------------------------------------------------------------------------
+struct Dropout {
+  uint32_t lseed;   // per step and BN layer
+  float rate;       // 0 = off
+  float scale;
+  int H;            // columns of the layer (17 * F)
+  int64_t row0;     // global row of local row 0 (rank offset)
+};
+__host__ __device__ inline uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x85ebca6bu; x ^= x >> 13; x *= 0xc2b2ae35u; x ^= x >> 16;
+  return x;
+}
+__host__ __device__ inline bool drop_keep(const Dropout& d, int64_t row, int col) {
+  const uint64_t key = (uint64_t)(d.row0 + row) * (uint64_t)d.H + (uint64_t)col;
+  const uint32_t x = fmix32(fmix32((uint32_t)key ^ d.lseed) + (uint32_t)(key >> 32));
+  return (float)(x >> 8) * 5.9604644775390625e-8f >= d.rate;
+}
+// x * scale if kept, else 0
+__host__ __device__ inline float drop_apply(const Dropout& d, int64_t row, int col, float x) {
+  return drop_keep(d, row, col) ? x * d.scale : 0.f;
+}
+
+// ----------------------------------------------------------------------------
 // Block-sparse GEMM (forward z = a.We + b and backward dA = dZ.We^T).
 // Output slab `so` of a row tile accumulates X[:, si-slab] . blocks[blk] over
 // the (si, blk) list ptr[so]..ptr[so+1].
@@ -74,6 +106,7 @@ struct GemmArgs {
   const float* epi_z;                // EPI_BNBACK: z of the layer below (tiled like Y)
   const float* epi_scale; const float* epi_shift; const float* epi_mean; const float* epi_rstd;
   int epi_F;                         // channels of the epi_* vectors (spj of Y = epi_F/64)
+  Dropout epi_drop;                  // EPI_BNBACK: dropout of the layer below (rate 0 = off)
   int B; int n_out_slabs; int n_rt;  // n_rt = ceil(B / 32)
 };
 void launch_gemm_bs(const GemmArgs& a, hipStream_t s);
@@ -88,6 +121,7 @@ struct GemmDwArgs {
   int d_bnback; int spj_d;
   const float* d_z; const float* d_scale; const float* d_shift; const float* d_c123; int d_F;
   float* dz_out;                     // d_bnback: dz (tiled like D) or null
+  Dropout d_drop;                    // d_bnback: dropout of D's layer (rate 0 = off)
   const int2* blk;                   // (si, so) per block
   int nblk;
   const int4* groups; int ngroups;   // block groups (see above)
@@ -178,7 +212,8 @@ void launch_bn_bwd_finalize(const double2* col, int H, int F, int phase, int bn,
                             float* c123, const double* zsum, float* db, hipStream_t s);
 // h = [res +] leaky(scale*z + shift), tiled [B][S*64] buffers
 void launch_bn_act(const float* z, const float* res, float* h, const float* scale,
-                   const float* shift, int F, float alpha, int B, int S, hipStream_t s);
+                   const float* shift, int F, float alpha, int B, int S, const Dropout& drop,
+                   hipStream_t s);
 // per-kEwRows-tile column sums of a 1-slab tiled src (ncols <= 64 used) ->
 // part[tiles][ncols] as (sum, 0)
 void launch_colpart(const float* src, int B, int ncols, float2* part, hipStream_t s);

@@ -83,6 +83,7 @@ SIGNATURES = {
     "lcn_comm_init": ([_vp, _vp, _i32, _i32], _i32),
     "lcn_comm_allreduce_host": ([_vp, _f64p, _i32, _i32], _i32),
     "lcn_crc32c": ([ctypes.c_uint32, ctypes.c_char_p, _i64], ctypes.c_uint32),
+    "lcn_set_dropout": ([_vp, ctypes.c_float, ctypes.c_uint64], _i32),
     "lcn_eval_mpjpe": ([_i32, _i64, _f64p, _f64p, _f64p, _f64p, _f64p, _i32, _f64p], _i32),
     "lcn_set_timing": ([_vp, _i32], _i32),
     "lcn_kernel_timing": ([_vp, _i32, _i64p, _f64p, _f64p], _i32),
@@ -374,6 +375,11 @@ class Network:
         return v
 
     # -- instrumentation
+    def set_dropout(self, rate: float, seed: int = 0):
+        """tf.nn.dropout(rate) in training steps (lcn_set_dropout); 0 = off.
+        The step counter of the masks restarts at 0."""
+        self._check(self.lib.lcn_set_dropout(self.h, float(rate), int(seed) & (2 ** 64 - 1)))
+
     def set_timing(self, enable: bool):
         self._check(self.lib.lcn_set_timing(self.h, int(enable)))
 

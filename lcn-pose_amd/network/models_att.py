@@ -7,6 +7,8 @@ The TensorFlow graph + Session is replaced by liblcn.so (HIP kernels for
 gfx950) through lcn_amd.native; there is no CPU compute path.
 
 Deliberate differences from the reference, all documented in DESIGN.md:
+  * dropout masks come from liblcn's counter-based generator (TF's random
+    stream cannot be reproduced); rate, scaling and placement are TF's;
   * resuming from a checkpoint restores the weights AND keeps them (the
     reference re-runs the initializer after restoring, :177-180);
   * checkpoints are TensorFlow tensor bundles written without TensorFlow
@@ -139,9 +141,6 @@ class base_model(object):
     def fit(self, train_data, train_labels, val_data, val_labels, output_dir=None,
             starting_checkpoint=None):
         """Training loop of models_att.py:148-286 (one lcn_train_step per step)."""
-        if self.dropout not in (0, None, 0.0):
-            # predict feeds dropout 0 (:102), so only training is affected
-            raise NotImplementedError("training with dropout > 0 is not implemented on the MI355X path yet")
         t_process, t_wall = time.process_time(), time.time()
         starting_step = 1
         net = self._net
@@ -166,6 +165,12 @@ class base_model(object):
             if ema is not None:
                 self._loss_ema = list(ema)
 
+        # tf.nn.dropout in the training graph only (fit feeds self.dropout,
+        # :204; predict feeds 0, :102).  The masks come from liblcn's
+        # counter-based generator, seeded outside numpy's global stream so the
+        # batch permutations stay the reference's draws
+        seed = int(os.environ.get("LCN_DROPOUT_SEED", int.from_bytes(os.urandom(8), "little")))
+        net.set_dropout(float(self.dropout or 0.0), seed)
         losses = []
         # the deque of np.random.permutation() indices of :193-200, kept as an
         # array (same draws, same order); the arrays themselves live in HBM

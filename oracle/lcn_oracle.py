@@ -255,8 +255,47 @@ def _act(cfg, u):
     return np.where(u > 0, u, u * u.dtype.type(cfg.leaky_alpha))
 
 
-def forward(cfg: Config, params, x: np.ndarray, dtype=np.float32, keep: bool = True):
-    """_inference_lcn (models_att.py:707-775).  Returns (out, cache)."""
+def _fmix32(x):
+    x = np.asarray(x, np.uint32)
+    x = x ^ (x >> np.uint32(16))
+    x = x * np.uint32(0x85EBCA6B)
+    x = x ^ (x >> np.uint32(13))
+    x = x * np.uint32(0xC2B2AE35)
+    return x ^ (x >> np.uint32(16))
+
+
+def dropout_mask(rate, seed, step, k, B, H, row0=0):
+    """Keep mask [B, H] of BN layer k's dropout in training step ``step``
+    after lcn_set_dropout(rate, seed) -- the counter-based hash of
+    lcn_internal.h (Dropout, drop_keep) and lcn_api.cpp (run_train_step,
+    drop_of).  Not TF's random stream (which cannot be reproduced); TF's
+    dropout semantics (models_att.py:673, 700, 742): keep iff u >= rate with
+    u uniform in [0, 1), kept values scaled by float32(1 / (1 - rate))."""
+    with np.errstate(over="ignore"):
+        s32 = np.uint32((int(seed) ^ (int(seed) >> 32)) & 0xFFFFFFFF)
+        step_seed = _fmix32(s32 + _fmix32(np.uint32((step + 0x9E3779B9) & 0xFFFFFFFF)))
+        lseed = _fmix32(step_seed ^ np.uint32(((k + 1) * 0x9E3779B9) & 0xFFFFFFFF))
+        key = ((np.arange(B, dtype=np.uint64)[:, None] + np.uint64(row0)) * np.uint64(H)
+               + np.arange(H, dtype=np.uint64)[None, :])
+        lo = (key & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        hi = (key >> np.uint64(32)).astype(np.uint32)
+        xh = _fmix32(_fmix32(lo ^ lseed) + hi)
+    u = (xh >> np.uint32(8)).astype(np.float32) * np.float32(2.0 ** -24)
+    return u >= np.float32(rate)
+
+
+def dropout_scale(rate):
+    """TF: 1 / (1 - rate) in float32."""
+    return np.float32(1) / (np.float32(1) - np.float32(rate))
+
+
+def forward(cfg: Config, params, x: np.ndarray, dtype=np.float32, keep: bool = True,
+            drop: Optional[Tuple[float, int, int]] = None):
+    """_inference_lcn (models_att.py:707-775).  Returns (out, cache).
+
+    ``drop`` = (rate, seed, step): the training graph's tf.nn.dropout after
+    every BN + LeakyReLU (models_att.py:673, 700, 742) with the masks of
+    dropout_mask."""
     P = {k: np.asarray(v, dtype) for k, v in params.items()}
     x = np.asarray(x, dtype)
     B = x.shape[0]
@@ -275,8 +314,13 @@ def forward(cfg: Config, params, x: np.ndarray, dtype=np.float32, keep: bool = T
         else:
             u, st = z, None
         h = _act(cfg, u)
+        m = None
+        if drop is not None and drop[0] > 0:
+            m = dropout_mask(drop[0], drop[1], drop[2], li, B, fout * J)
+            h = np.where(m, h * h.dtype.type(dropout_scale(drop[0])), h.dtype.type(0))
         if keep:
-            cache["layers"].append(dict(a=a, z=z, u=u, st=st))
+            cache["layers"].append(dict(a=a, z=z, u=u, st=st, m=m,
+                                        scale=dropout_scale(drop[0]) if m is not None else None))
         return h, z, st
 
     h, _, _ = linear_bn_act(x, 0)                          # :729-742
@@ -327,6 +371,8 @@ def _bn_act_backward(cfg, dh, rec, F, gamma, pos=None):
     than the float64 one takes the other branch of the kink."""
     B = dh.shape[0]
     u = rec["u"]
+    if rec.get("m") is not None:  # tf.nn.dropout's gradient: dh * mask * scale
+        dh = np.where(rec["m"], dh * dh.dtype.type(rec["scale"]), dh.dtype.type(0))
     if pos is None:
         pos = u > 0
     du = dh * np.where(pos, dh.dtype.type(1), dh.dtype.type(cfg.leaky_alpha))

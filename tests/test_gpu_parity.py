@@ -211,3 +211,38 @@ def test_cfg4_shape_matches_oracle():
     bad = {k: rel_err(g[k], ref[k]) for k, _ in O.param_specs(cfg) if rel_err(g[k], ref[k]) > 1e-4}
     print(f"kink branch disagreements: {flips}")
     assert not bad, bad
+
+
+@pytest.mark.parametrize("L,B,rate", [(3, 256, 0.3), (1, 200, 0.25)])
+def test_dropout_training_step_matches_oracle(L, B, rate):
+    """tf.nn.dropout after every BN + LeakyReLU (models_att.py:673, 700, 742)
+    with the counter-based masks (oracle.dropout_mask): loss and every
+    gradient of two consecutive training steps (mask step 0, then 1) against
+    the float64 oracle; predict is unaffected by the dropout setting."""
+    cfg, params, x, lab, net = _setup(dict(F=64, L=L, knn=3), B)
+    seed = 0x1234_5678_9ABC
+    net.set_dropout(rate, seed)
+    for step in range(2):
+        loss, _ = net.train_step(x, lab, update=False, keep_grads=True)
+        g = O.unflatten(cfg, net.get_grads())
+        kinks = _device_kinks(cfg, params, net, B)  # see test_cfg4_shape_matches_oracle
+        out64, cache = O.forward(cfg, params, x, np.float64, drop=(rate, seed, step))
+        assert abs(loss - O.mse_loss(out64, lab)) <= 1e-5 * abs(loss)
+        for k, pos in kinks.items():
+            u = cache["layers"][k]["u"]
+            d = pos != (u > 0)
+            assert d.sum() <= 2 and (not d.any() or np.abs(u[d]).max() <= 1e-4 * np.sqrt(np.mean(u * u)))
+        ref = O.backward(cfg, params, cache, lab, np.float64, kinks=kinks)
+        out32, c32 = O.forward(cfg, params, x, np.float32, drop=(rate, seed, step))
+        ref32 = O.backward(cfg, params, c32, lab, np.float32, kinks=kinks)
+        bad = {}
+        for k, _ in O.param_specs(cfg):
+            e, tol = rel_err(g[k], ref[k]), max(1e-4, 2.0 * rel_err(ref32[k], ref[k]))
+            if e > tol:
+                bad[k] = (e, tol)
+        assert not bad, (step, bad)
+    ref_plain, _ = O.forward(cfg, params, x, np.float64)
+    assert np.abs(net.forward(x) - ref_plain).max() <= 1e-4
+    net.set_dropout(0.0)
+    loss0, _ = net.train_step(x, lab, update=False)
+    assert abs(loss0 - O.mse_loss(ref_plain, lab)) <= 1e-5 * abs(loss0)

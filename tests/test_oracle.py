@@ -101,8 +101,10 @@ def _small_cfg(mask="locally_connected", **kw):
                                      ("exponential", {}),
                                      ("locally_connected", {"residual": False, "in_F": 3}),
                                      ("locally_connected", {"batch_norm": False}),
-                                     ("locally_connected", {"regularization": 0.01})])
+                                     ("locally_connected", {"regularization": 0.01}),
+                                     ("locally_connected", {"dropout": (0.3, 77, 2)})])
 def test_backward_matches_finite_differences(mask, kw):
+    drop = kw.pop("dropout", None)
     cfg = _small_cfg(mask, **kw)
     params = {k: v.astype(np.float64) for k, v in O.init_params(cfg, seed=5).items()}
     if "mask" in params:  # break the symmetric init so softmax gradients are generic
@@ -113,10 +115,10 @@ def test_backward_matches_finite_differences(mask, kw):
     lab = rng.uniform(-1, 1, size=(B, 51))
 
     def loss_of(p):
-        out, _ = O.forward(cfg, p, x, np.float64)
+        out, _ = O.forward(cfg, p, x, np.float64, drop=drop)
         return O.mse_loss(out, lab) + O.reg_loss(cfg, p)
 
-    out, cache = O.forward(cfg, params, x, np.float64)
+    out, cache = O.forward(cfg, params, x, np.float64, drop=drop)
     grads = O.backward(cfg, params, cache, lab, np.float64)
     rs = np.random.default_rng(11)
     for name, shape in O.param_specs(cfg):
@@ -199,3 +201,23 @@ def test_adam_matches_closed_form():
     # first step: m = 0.1 g, v = 0.001 g^2, alpha = lr*sqrt(0.001)/0.1 -> step = lr*sign(g)
     np.testing.assert_allclose(params["a"], [1.0 - 1e-3, -2.0 + 1e-3], rtol=1e-5)
     assert st.global_step == 1 and st.beta1_power == np.float32(0.9) * np.float32(0.9)
+
+
+def test_dropout_masks():
+    """Counter-based dropout masks (lcn_internal.h Dropout): the kept fraction
+    is 1 - rate, masks differ across layers, steps, seeds and rows, and
+    rate 0 keeps everything; the scale is TF's float32 1 / (1 - rate)."""
+    B, H = 512, 1088
+    for rate in (0.25, 0.3, 0.5):
+        m = O.dropout_mask(rate, 123, 0, 1, B, H)
+        assert abs(m.mean() - (1 - rate)) < 4 * np.sqrt(rate * (1 - rate) / m.size)
+    a = O.dropout_mask(0.3, 123, 0, 1, B, H)
+    for other in (O.dropout_mask(0.3, 123, 0, 2, B, H), O.dropout_mask(0.3, 123, 1, 1, B, H),
+                  O.dropout_mask(0.3, 124, 0, 1, B, H), O.dropout_mask(0.3, 123, 0, 1, B, H, row0=B)):
+        agree = (a == other).mean()
+        assert abs(agree - (0.7 ** 2 + 0.3 ** 2)) < 0.01, agree   # independent masks
+    assert O.dropout_mask(0.0, 5, 3, 0, 8, 64).all()
+    assert O.dropout_scale(0.3) == np.float32(1) / (np.float32(1) - np.float32(0.3))
+    # row0 shifts rows: the second half of a 2B batch is the B batch at row0 = B
+    np.testing.assert_array_equal(O.dropout_mask(0.3, 9, 4, 3, 2 * B, H)[B:],
+                                  O.dropout_mask(0.3, 9, 4, 3, B, H, row0=B))
