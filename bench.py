@@ -208,6 +208,27 @@ def main():
                 "achieved": round(d["tflops"], 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(d["tflops"] / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
                 "avg_launch_ms": round(d["avg_ms"], 4)}
+        # the metric's "achieved HBM GB/s vs peak", for the hidden-layer forward
+        # GEMM (the north star's fused LCN forward): algorithmic bytes = read the
+        # input activations + write z, 2 x 17*F floats per pose
+        hbm = None
+        if "gemm_fwd" in kern:
+            f = kern["gemm_fwd"]
+            alg = 2 * 17 * args.channels * 4 * B
+            tr = None
+            if os.path.exists(args.traffic_file):
+                try:
+                    tr = json.load(open(args.traffic_file)).get("gemm_fwd", {}).get("hbm_bytes_per_launch")
+                except Exception:
+                    tr = None
+            ach = alg / (f["avg_ms"] * 1e-3) / 1e9
+            hbm = {"kernel": "gemm_fwd (hidden-layer forward: masked GEMM + bias + BN statistics, "
+                             "BN apply + LeakyReLU of its input fused)",
+                   "algorithmic_bytes": alg, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                   "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr,
+                   "traffic_GBps": round(tr / (f["avg_ms"] * 1e-3) / 1e9, 1) if tr else None,
+                   "mfma_frac": round(f["tflops"] / FP32_PEAK_TFLOPS, 4),
+                   "note": "compute-bound: 165 FLOP/B vs a 19.7 FLOP/B fp32 ridge (DESIGN.md)"}
         res = {
             "metric": METRIC, "value": round(value, 1), "unit": "poses/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
@@ -218,6 +239,7 @@ def main():
                        "global_batch": B * world, "per_gpu_batch": B, "layers": args.layers,
                        "channels": args.channels, "parallelism": f"dp{world} (SyncBN + RCCL grad all-reduce)"},
             "roofline": roof,
+            "hbm": hbm,
             "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv for kk, vv in v.items()}
                         for k, v in kern.items()},
             "fwd_only_poses_per_s": round(B * world * nf / tfwd, 1),
