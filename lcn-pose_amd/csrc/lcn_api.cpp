@@ -214,7 +214,12 @@ int upload_dw_groups(Handle* h, const std::vector<int2>& blk, int4** dev, int* n
 }
 
 // batch chunks of the weight-gradient GEMM: ~8k workgroups in total, <= 64 chunks
-int dw_chunks(int nblk) { return std::max(1, std::min(64, 8192 / std::max(1, nblk))); }
+// batch chunks of a weight-gradient launch (partials per block = chunks);
+// LCN_DW_ROWS overrides the block-rows budget (tuning runs)
+int dw_chunks(int nblk) {
+  static const int budget = std::getenv("LCN_DW_ROWS") ? std::atoi(std::getenv("LCN_DW_ROWS")) : 5600;
+  return std::max(1, std::min(64, budget / std::max(1, nblk)));
+}
 
 // ---------------------------------------------------------------------------
 // construction
