@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--mode", choices=["train", "predict"], default="train",
+                    help="train: the headline training step (default); predict: cfg5-style "
+                         "inference -- float64 poses resident in HBM, flip + rotation TTA "
+                         "(3 copies), batch-statistics BN, undo + average on the device")
     return ap.parse_args()
 
 
@@ -111,8 +115,52 @@ def cpu_baseline(args, seconds):
                       f"{len(times)} steps, median {med:.3f} s/step, OpenBLAS threads={cores}"}
 
 
+def predict_main(args, rank, world, local):
+    """BASELINE.json configs[4] shape (cfg5): TTA predict of `--batch` poses per
+    GPU (flip + rotation: 3 copies, inference.py:70-111) through
+    lcn_predict_dataset, batch size = --batch, float64 predictions to the host."""
+    from lcn_amd.tta import augment_ops
+    B = args.batch
+    neighbour = get_neighbour_matrix_by_hand(neighbour_dict_set[0], knn=args.knn)
+    mask = (neighbour.T != 0).astype(np.float32)
+    net = native.Network(F=args.channels, in_F=2, num_layers=args.layers, mask_type=args.mask_type,
+                         mask_matrix=mask, max_batch=B, device=local)
+    if world > 1:
+        net.comm_init(exchange_uid(rank, world), rank, world)
+    net.set_params(init_flat(net.param_layout(), net.n_params, neighbour, seed=0))
+    rng = np.random.default_rng(99 + rank)
+    x = rng.uniform(-1, 1, (B, 34))                      # float64, as DataReader yields
+    net.dataset_upload(0, x)
+    aug, undo, _ = augment_ops(flip=True, rotate=True)
+    for _ in range(args.warmup):
+        net.predict_dataset(0, B, B, augment=aug, undo=undo)
+    net.allreduce_host([0.0])
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pred = net.predict_dataset(0, B, B, augment=aug, undo=undo)
+    net.synchronize()
+    net.allreduce_host([0.0])
+    el = float(net.allreduce_host([time.perf_counter() - t0], op="max")[0])
+    if rank == 0:
+        print(json.dumps({
+            "metric": "poses/sec, TTA predict (flip + rotation, 3 copies per pose)",
+            "value": round(B * world * args.steps / el, 1), "unit": "poses/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic float64 poses resident in HBM; predictions float64 to the host",
+            "config": {"workload": f"cfg5-style inference: locally_connected knn={args.knn}, "
+                                   f"layers={args.layers}, F={args.channels}, flip+rotation TTA",
+                       "poses_per_gpu": B, "network_batch": B, "copies": 3,
+                       "parallelism": f"dp{world} (SyncBN over the ranks' batches)"},
+            "finite": bool(np.isfinite(pred).all())}), flush=True)
+    net.close()
+
+
 def main():
     args = parse()
+    if args.mode == "predict":
+        rank, world, local = dist_env()
+        return predict_main(args, rank, world, local)
     rank, world, local = dist_env()
     if world != args.gpus:
         # launched without torchrun: single process drives one GPU
