@@ -113,7 +113,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   const float al = a.alpha;
   const float* tsc = nullptr;
   const float* tsh = nullptr;
-  if constexpr (PRO == PRO_BNACT) {
+  const int spj = a.spj_in;
+  constexpr int DSR = PRO == PRO_BNACT ? 4 : 2;  // LDS reads per k-group
+
+  // the first weight block and activation fragments go in flight first; the
+  // bias / residual / table loads below are batched behind them, so the
+  // prologue waits for memory once (not once per accumulator quarter)
+  const int S_out = a.S_out, ncols = S_out * kSlab;
+  const size_t tbase = ((size_t)rt * S_out + so) * 512 + lane;  // float4 index of chunk 0
+  DECLX(xa)
+  DECLX(xb)
+  int2 ia = idx[beg], ib = ia;
+  LOADW(ia.y, 0)
+  LOADX(xa, ia.x)
+  // accumulators start at bias + residual (the MFMAs add onto them)
+  float4 bq[8], rq[8];
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.bias) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) bq[q] = *(const float4*)(a.bias + so * kSlab + 8 * q + 4 * h);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) bq[q] = zero4;
+  }
+  if (a.addsrc) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) rq[q] = ((const float4*)a.addsrc)[tbase + q * 64];
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) rq[q] = zero4;
+  }
+  if constexpr (PRO == PRO_BNACT) {  // BN scale / shift of the operand's layer -> LDS
     float* tb = (float*)(Wl + 2048);
     for (int c = threadIdx.x; c < a.pro_F; c += 256) {
       tb[c] = a.pro_scale[c];
@@ -122,31 +152,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
     tsc = tb;
     tsh = tb + a.pro_F;
   }
-  const int spj = a.spj_in;
-  constexpr int DSR = PRO == PRO_BNACT ? 4 : 2;  // LDS reads per k-group
-
-  // accumulators start at bias + residual (the MFMAs add onto them)
-  const int S_out = a.S_out, ncols = S_out * kSlab;
-  const size_t tbase = ((size_t)rt * S_out + so) * 512 + lane;  // float4 index of chunk 0
-  f32x16 acc0, acc1;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
-    if (a.bias) {
-      b0 = *(const float4*)(a.bias + so * kSlab + 8 * q + 4 * h);
-      b1 = *(const float4*)(a.bias + so * kSlab + 32 + 8 * q + 4 * h);
-    }
-    if (a.addsrc) {
-      const float4 r0 = ((const float4*)a.addsrc)[tbase + q * 64];
-      const float4 r1 = ((const float4*)a.addsrc)[tbase + (4 + q) * 64];
-      b0.x += r0.x; b0.y += r0.y; b0.z += r0.z; b0.w += r0.w;
-      b1.x += r1.x; b1.y += r1.y; b1.z += r1.z; b1.w += r1.w;
-    }
-    acc0[4 * q + 0] = b0.x; acc0[4 * q + 1] = b0.y; acc0[4 * q + 2] = b0.z; acc0[4 * q + 3] = b0.w;
-    acc1[4 * q + 0] = b1.x; acc1[4 * q + 1] = b1.y; acc1[4 * q + 2] = b1.z; acc1[4 * q + 3] = b1.w;
-  }
-  // EPI_BNBACK reads z of the layer below: fetched now, used after the loop;
-  // the per-channel BN constants of this output slab go to an LDS table
+  // EPI_BNBACK reads z of the layer below after the loop; the per-channel BN
+  // constants of this output slab go to an LDS table
   float4 zp0, zp1, zp2, zp3, zp4, zp5, zp6, zp7;
   float* ptab = (float*)(Wl + 2048);  // [4][64]: scale, shift, mean, rstd
   if constexpr (EPI == EPI_BNBACK) {
@@ -154,11 +161,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
     const float* src = pk == 0 ? a.epi_scale : pk == 1 ? a.epi_shift : pk == 2 ? a.epi_mean : a.epi_rstd;
     ptab[threadIdx.x] = src[ch];
   }
-  DECLX(xa)
-  DECLX(xb)
-  int2 ia = idx[beg], ib = ia;
-  LOADW(ia.y, 0)
-  LOADX(xa, ia.x)
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 b0 = bq[q], b1 = bq[4 + q], r0 = rq[q], r1 = rq[4 + q];
+    acc0[4 * q + 0] = b0.x + r0.x; acc0[4 * q + 1] = b0.y + r0.y;
+    acc0[4 * q + 2] = b0.z + r0.z; acc0[4 * q + 3] = b0.w + r0.w;
+    acc1[4 * q + 0] = b1.x + r1.x; acc1[4 * q + 1] = b1.y + r1.y;
+    acc1[4 * q + 2] = b1.z + r1.z; acc1[4 * q + 3] = b1.w + r1.w;
+  }
   __syncthreads();
   // every output slab has >= 1 input block (checked in lcn_create)
   for (int e = beg; e < end; e += 2) {
