@@ -29,7 +29,7 @@ namespace lcn {
 // costs one write and no separate elementwise pass.
 constexpr int kDwLd = 36;
 
-template <bool PRO, bool DBB>
+template <bool PRO, bool DBB, bool DROP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gemm_dw_kernel(GemmDwArgs a) {
   __shared__ __attribute__((aligned(16))) float Ds[64 * kDwLd];      // [q][row]
   __shared__ __attribute__((aligned(16))) float As[2][64 * kDwLd];   // [p][row] per block
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
         c.c3 = *(const float4*)(tab + 512 + f);
         return c;
       };
-      if (a.d_drop.rate > 0.f) {  // tf.nn.dropout's gradient: dh * mask * scale
+      if constexpr (DROP) {  // tf.nn.dropout's gradient: dh * mask * scale
         const int64_t row = base + lr;
         const int col = so * kSlab + f0;
         rd0.x = drop_apply(a.d_drop, row, col, rd0.x);
@@ -187,14 +187,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
 void launch_gemm_dw(const GemmDwArgs& a, hipStream_t s) {
   const int grid = a.ngroups * a.nchunks;
   const bool pro = a.pro_scale != nullptr, dbb = a.d_bnback != 0;
-  if (pro && dbb)
-    hipLaunchKernelGGL((gemm_dw_kernel<true, true>), dim3(grid), dim3(256), 0, s, a);
+  // the dropout variants are separate instances: the mask hash costs registers
+  const bool drop = dbb && a.d_drop.rate > 0.f;
+  if (pro && drop)
+    hipLaunchKernelGGL((gemm_dw_kernel<true, true, true>), dim3(grid), dim3(256), 0, s, a);
+  else if (drop)
+    hipLaunchKernelGGL((gemm_dw_kernel<false, true, true>), dim3(grid), dim3(256), 0, s, a);
+  else if (pro && dbb)
+    hipLaunchKernelGGL((gemm_dw_kernel<true, true, false>), dim3(grid), dim3(256), 0, s, a);
   else if (pro)
-    hipLaunchKernelGGL((gemm_dw_kernel<true, false>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw_kernel<true, false, false>), dim3(grid), dim3(256), 0, s, a);
   else if (dbb)
-    hipLaunchKernelGGL((gemm_dw_kernel<false, true>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw_kernel<false, true, false>), dim3(grid), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((gemm_dw_kernel<false, false>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw_kernel<false, false, false>), dim3(grid), dim3(256), 0, s, a);
 }
 
 // Sum the chunk partials of every block in a fixed order and scatter into the
@@ -223,3 +229,4 @@ void launch_dw_reduce(const float* part, int nchunks, int nblk, const int2* blk,
 }
 
 }  // namespace lcn
+

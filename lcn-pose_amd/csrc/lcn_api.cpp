@@ -101,6 +101,7 @@ struct Handle {
   // weight-gradient work groups (kernels_gemm.hip): up to 2 blocks sharing an output slab
   int4 *grp_hidden = nullptr, *grp_lift = nullptr, *grp_out = nullptr;
   int ngrp_hidden = 0, ngrp_lift = 0, ngrp_out = 0;
+
   std::vector<BnStats> bn;
   std::vector<double*> zsum;      // per BN layer: column sums of z (bias-gradient term)
   float *ident_scale = nullptr, *ident_shift = nullptr, *ident_c123 = nullptr;
@@ -213,7 +214,6 @@ int upload_dw_groups(Handle* h, const std::vector<int2>& blk, int4** dev, int* n
   return upload(h, dev, g);
 }
 
-// batch chunks of the weight-gradient GEMM: ~8k workgroups in total, <= 64 chunks
 // batch chunks of a weight-gradient launch (partials per block = chunks);
 // LCN_DW_ROWS overrides the block-rows budget (tuning runs)
 int dw_chunks(int nblk) {
