@@ -96,6 +96,10 @@ namespace lcn {
   GSTEP(BUF, 3, P##3, CH) GSTEP(BUF, 4, P##4, CH) GSTEP(BUF, 5, P##5, CH) \
   GSTEP(BUF, 6, P##6, CH) GSTEP(BUF, 7, P##7, CH) SCHED_SLAB
 
+// EPI_BNBACK with the dropout of the layer below: a separate instance, since
+// the mask hash costs the plain kernel registers (it spilled)
+constexpr int kEpiBnBackDrop = 3;
+
 template <int PRO, int EPI>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gemm_bs_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) float4 Wl[];  // [2][1024] (+ BN tables)
@@ -156,7 +160,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   // constants of this output slab go to an LDS table
   float4 zp0, zp1, zp2, zp3, zp4, zp5, zp6, zp7;
   float* ptab = (float*)(Wl + 2048);  // [4][64]: scale, shift, mean, rstd
-  if constexpr (EPI == EPI_BNBACK) {
+  if constexpr (EPI == EPI_BNBACK || EPI == kEpiBnBackDrop) {
     const int pk = threadIdx.x >> 6, ch = (so % (a.epi_F / kSlab)) * kSlab + lane;
     const float* src = pk == 0 ? a.epi_scale : pk == 1 ? a.epi_shift : pk == 2 ? a.epi_mean : a.epi_rstd;
     ptab[threadIdx.x] = src[ch];
@@ -194,7 +198,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   }
 
   // ---- epilogue ----
-  if constexpr (EPI == EPI_BNBACK) {
+  if constexpr (EPI == EPI_BNBACK || EPI == kEpiBnBackDrop) {
     // z of the layer below, issued before the output stores so its latency
     // overlaps them (keeping it live through the loop would cost 32 VGPRs,
     // i.e. a wave per SIMD of occupancy)
@@ -276,7 +280,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   // below; pass 0 reduces du, pass 1 du * zhat
   // dropout of the layer below (tf.nn.dropout's gradient: dh * mask * scale),
   // applied to the partials only -- the stored dh stays the incoming gradient
-  if (a.epi_drop.rate > 0.f) {
+  if constexpr (EPI == kEpiBnBackDrop) {
     const int64_t row = (int64_t)rt * kRT + (lane & 31);
 #pragma unroll
     for (int i = 0; i < 32; ++i) v[i] = drop_apply(a.epi_drop, row, so * kSlab + acc_feature(i, h), v[i]);
@@ -336,6 +340,7 @@ void launch_gemm_bs(const GemmArgs& a, hipStream_t s) {
     else LAUNCH(PRO_BNACT, EPI_NONE, ldsp);
   } else {
     if (a.epi_mode == EPI_BNFWD) LAUNCH(PRO_RAW, EPI_BNFWD, ldse);
+    else if (a.epi_mode == EPI_BNBACK && a.epi_drop.rate > 0.f) LAUNCH(PRO_RAW, kEpiBnBackDrop, ldse);
     else if (a.epi_mode == EPI_BNBACK) LAUNCH(PRO_RAW, EPI_BNBACK, ldse);
     else LAUNCH(PRO_RAW, EPI_NONE, lds);
   }
