@@ -240,8 +240,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ theta, fl
                                                    const int64_t* __restrict__ seg_start, int nseg,
                                                    const float* __restrict__ M,
                                                    const float* __restrict__ lcoef, float reg,
-                                                   float lr_t, float beta1, float beta2, float eps,
-                                                   int update) {
+                                                   const float* __restrict__ lr_t_dev, float beta1,
+                                                   float beta2, float eps, int update) {
   const int64_t b = blockIdx.x;
   int lo = 0, hi = nseg - 1;
   while (lo < hi) {
@@ -251,6 +251,9 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ theta, fl
   const AdamSeg sg = segs[lo];
   const int64_t base = (b - seg_start[lo]) * 1024;
   const float omb1 = 1.f - beta1, omb2 = 1.f - beta2;
+  // lr_t = lr * sqrt(1 - beta2^t) / (1 - beta1^t), computed by the host per
+  // step and written to device memory (so a captured step graph replays it)
+  const float lr_t = *lr_t_dev;
   for (int k = 0; k < 4; ++k) {
     const int64_t e = base + k * 256 + threadIdx.x;
     if (e >= sg.size) break;
@@ -277,10 +280,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ theta, fl
 
 void launch_adam(float* theta, float* m, float* v, const float* rg, float* gout,
                  const AdamSeg* segs, const int64_t* seg_block_start, int nseg,
-                 int64_t total_blocks, const float* M, const float* lcoef, float reg, float lr_t,
-                 float beta1, float beta2, float eps, int update, hipStream_t s) {
+                 int64_t total_blocks, const float* M, const float* lcoef, float reg,
+                 const float* lr_t_dev, float beta1, float beta2, float eps, int update, hipStream_t s) {
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)total_blocks), dim3(256), 0, s, theta, m, v, rg,
-                     gout, segs, seg_block_start, nseg, M, lcoef, reg, lr_t, beta1, beta2, eps,
+                     gout, segs, seg_block_start, nseg, M, lcoef, reg, lr_t_dev, beta1, beta2, eps,
                      update);
 }
 

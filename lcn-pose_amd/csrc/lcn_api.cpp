@@ -145,6 +145,13 @@ struct Handle {
 
   // instrumentation
   int timing = 0;
+  // train-step graphs (world 1, no dropout, no timing): the device work of a
+  // step captured once per (batch, update, keep_grads) and replayed -- small
+  // batches are launch-bound (fit's reference batch is 200)
+  struct StepGraph { int64_t B; bool update, keep; hipGraphExec_t exec; };
+  std::vector<StepGraph> graphs;
+  int use_graphs = 0;  // LCN_GRAPHS=1 turns them on (rocprofv3 kernel tracing crashed on graph launches)
+  float* lr_dev = nullptr;  // Adam's lr_t of the running step
   Timer timers[LCN_K_NUM];
 
   std::vector<void*> allocs;
@@ -440,6 +447,8 @@ int build(Handle* h, const lcn_config* c) {
   CHECK(dalloc(h, &h->DH, tH));
   CHECK(dalloc(h, &h->DG, tH));
   CHECK(dalloc(h, &h->DZ, tH));
+  CHECK(dalloc(h, &h->lr_dev, 1));
+  if (const char* g = std::getenv("LCN_GRAPHS")) h->use_graphs = std::atoi(g) != 0;
   h->zsum.assign(nl - 1, nullptr);
   for (auto& zs : h->zsum) CHECK(dalloc(h, &zs, (size_t)H));
   h->nbn = nl - 1;
@@ -799,7 +808,8 @@ int backward(Handle* h, int B) {
   return LCN_OK;
 }
 
-int finish_and_update(Handle* h, bool update, bool keep_grads) {
+// the device side of the update: mask / clip backward, Adam (lr_t from lr_dev)
+int finish_device(Handle* h, bool update, bool keep_grads) {
   hipStream_t s = h->stream;
   if (h->world > 1) {
     CHECK(allreduce(h, h->rg, (size_t)h->P, ncclFloat));
@@ -807,17 +817,9 @@ int finish_and_update(Handle* h, bool update, bool keep_grads) {
   launch_wdot(h->rg, h->theta, h->w_offs, h->w_kin, h->w_nout, h->nl, h->blocksum, s);
   launch_maskgrad(h->blocksum, h->nl, h->Md, h->Sd, h->Cd, h->learnable, h->denom, h->norm2,
                   h->max_norm, h->learnable ? h->rg + h->mask_off : nullptr, h->lcoef, s);
-  const float lr = h->lr0 * powf(h->decay_rate, (float)h->global_step / (float)h->decay_steps);
-  const float lr_t = lr * sqrtf(1.f - h->b2p) / (1.f - h->b1p);
   launch_adam(h->theta, h->m, h->v, h->rg, keep_grads ? h->gout : nullptr, h->segs, h->seg_start,
-              h->nseg, h->adam_blocks, h->Md, h->lcoef, h->reg, lr_t, h->b1, h->b2, h->adam_eps,
+              h->nseg, h->adam_blocks, h->Md, h->lcoef, h->reg, h->lr_dev, h->b1, h->b2, h->adam_eps,
               update ? 1 : 0, s);
-  if (keep_grads) h->grads_valid = 1;
-  if (update) {
-    h->b1p *= h->b1;
-    h->b2p *= h->b2;
-    h->global_step += 1;
-  }
   return LCN_OK;
 }
 
@@ -904,6 +906,7 @@ int lcn_destroy(void* handle) {
   if (h->comm) ncclCommDestroy(h->comm);
   for (auto& t : h->timers)
     for (auto e : t.ev) hipEventDestroy(e);
+  for (auto& g : h->graphs) hipGraphExecDestroy(g.exec);
   for (void* p : h->allocs) hipFree(p);
   for (void* p : h->user_bufs) if (p) hipFree(p);
   for (auto& d : h->datasets) if (d.ptr) hipFree(d.ptr);
@@ -1044,15 +1047,64 @@ int lcn_forward_loss(void* handle, const float* x, const float* labels, float* o
   return LCN_OK;
 }
 
-static int run_train_step(Handle* h, int64_t B, int32_t flags, float* loss_out, float* lr_out) {
-  const float lr = h->lr0 * powf(h->decay_rate, (float)h->global_step / (float)h->decay_steps);
-  // dropout masks of this step: seed of training step number drop_calls
-  h->step_seed = fmix32(h->drop_seed + fmix32((uint32_t)h->drop_calls + 0x9e3779b9u));
-  if (h->drop_rate > 0.f) h->drop_calls++;
+// forward, loss, backward and update of one step, enqueued on the stream
+static int enqueue_step(Handle* h, int64_t B, bool update, bool keep) {
   CHECK(forward(h, (int)B, true, true));
   if (h->world > 1) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
   CHECK(backward(h, (int)B));
-  CHECK(finish_and_update(h, !(flags & LCN_NO_UPDATE), (flags & LCN_KEEP_GRADS) != 0));
+  return finish_device(h, update, keep);
+}
+
+// the captured graph of enqueue_step for (B, update, keep), made on first use
+static int step_graph(Handle* h, int64_t B, bool update, bool keep, hipGraphExec_t* out) {
+  for (const auto& g : h->graphs)
+    if (g.B == B && g.update == update && g.keep == keep) { *out = g.exec; return LCN_OK; }
+  hipGraph_t graph = nullptr;
+  HIPC(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
+  const int rc = enqueue_step(h, B, update, keep);
+  const hipError_t ec = hipStreamEndCapture(h->stream, &graph);
+  if (rc != LCN_OK) { if (graph) hipGraphDestroy(graph); return rc; }
+  if (ec != hipSuccess) { h->err = std::string("step graph capture: ") + hipGetErrorString(ec); return LCN_E_HIP; }
+  hipGraphExec_t exec = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  hipGraphDestroy(graph);
+  if (ei != hipSuccess) { h->err = std::string("step graph instantiate: ") + hipGetErrorString(ei); return LCN_E_HIP; }
+  h->graphs.push_back(Handle::StepGraph{B, update, keep, exec});
+  *out = exec;
+  return LCN_OK;
+}
+
+static int run_train_step(Handle* h, int64_t B, int32_t flags, float* loss_out, float* lr_out) {
+  const float lr = h->lr0 * powf(h->decay_rate, (float)h->global_step / (float)h->decay_steps);
+  const float lr_t = lr * sqrtf(1.f - h->b2p) / (1.f - h->b1p);
+  const bool update = !(flags & LCN_NO_UPDATE), keep = (flags & LCN_KEEP_GRADS) != 0;
+  // dropout masks of this step: seed of training step number drop_calls
+  h->step_seed = fmix32(h->drop_seed + fmix32((uint32_t)h->drop_calls + 0x9e3779b9u));
+  if (h->drop_rate > 0.f) h->drop_calls++;
+  uint32_t lr_bits;
+  std::memcpy(&lr_bits, &lr_t, 4);
+  HIPC(hipMemsetD32Async((hipDeviceptr_t)h->lr_dev, (int)lr_bits, 1, h->stream));
+  hipGraphExec_t exec = nullptr;
+  if (h->use_graphs && h->world == 1 && !h->timing && h->drop_rate == 0.f &&
+      step_graph(h, B, update, keep, &exec) != LCN_OK) {
+    // capture unavailable: fall back to direct launches for this handle
+    std::fprintf(stderr, "liblcn: step graph disabled (%s)\n", h->err.c_str());
+    (void)hipGetLastError();
+    h->err.clear();
+    h->use_graphs = 0;
+    exec = nullptr;
+  }
+  if (exec) {
+    HIPC(hipGraphLaunch(exec, h->stream));
+  } else {
+    CHECK(enqueue_step(h, B, update, keep));
+  }
+  if (keep) h->grads_valid = 1;
+  if (update) {
+    h->b1p *= h->b1;
+    h->b2p *= h->b2;
+    h->global_step += 1;
+  }
   CHECK(finish_launches(h));
   if (lr_out) *lr_out = lr;
   CHECK(read_loss(h, B, loss_out));

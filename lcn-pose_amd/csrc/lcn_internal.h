@@ -266,6 +266,6 @@ struct AdamSeg {
 void launch_adam(float* theta, float* m, float* v, const float* rg, float* gout,
                  const AdamSeg* segs, const int64_t* seg_block_start, int nseg,
                  int64_t total_blocks, const float* M, const float* lcoef, float reg,
-                 float lr_t, float beta1, float beta2, float eps, int update, hipStream_t s);
+                 const float* lr_t_dev, float beta1, float beta2, float eps, int update, hipStream_t s);
 
 }  // namespace lcn

@@ -246,3 +246,30 @@ def test_dropout_training_step_matches_oracle(L, B, rate):
     net.set_dropout(0.0)
     loss0, _ = net.train_step(x, lab, update=False)
     assert abs(loss0 - O.mse_loss(ref_plain, lab)) <= 1e-5 * abs(loss0)
+
+
+def test_step_graphs_replay_the_direct_launches(monkeypatch):
+    """Training steps replayed from a captured HIP graph (world 1, no dropout)
+    give bit-identical losses, parameters and optimiser state to the same
+    steps launched kernel by kernel (LCN_GRAPHS=0), across batch sizes,
+    update / no-update and keep-grads variants."""
+    cfg = make_cfg(F=64, L=2, knn=3)
+    params = perturbed_params(cfg, seed=2)
+    nets = []
+    for g in ("1", "0"):
+        monkeypatch.setenv("LCN_GRAPHS", g)
+        n = make_network(cfg, max_batch=512)
+        n.set_params(O.flatten(cfg, params))
+        n.set_optimizer_state(np.zeros(n.n_params), np.zeros(n.n_params), 0, 0.9, 0.999)
+        nets.append(n)
+    for i, (B, upd, keep) in enumerate([(200, True, False), (200, True, False), (512, True, True),
+                                        (200, False, True), (200, True, False), (512, True, False)]):
+        x, lab = synthetic_batch(B, 2, seed=20 + i)
+        res = [n.train_step(x, lab, update=upd, keep_grads=keep) for n in nets]
+        assert res[0] == res[1], (i, res)
+        if keep:
+            np.testing.assert_array_equal(nets[0].get_grads(), nets[1].get_grads())
+    np.testing.assert_array_equal(nets[0].get_params(), nets[1].get_params())
+    s0, s1 = nets[0].get_optimizer_state(), nets[1].get_optimizer_state()
+    for a, b in zip(s0, s1):
+        np.testing.assert_array_equal(a, b)
