@@ -213,6 +213,7 @@ def main():
         if n:
             kern[name] = {"launches": n, "avg_ms": ms / n, "tflops": fl / (ms * 1e-3) / 1e12,
                           "total_ms_per_step": ms / args.steps}
+    bn_act_timing = net.kernel_timing(native.K_BN_ACT)
     net.set_timing(False)
 
     # forward-only rate (BASELINE configs[1], cfg2) on the same resident batch
@@ -259,6 +260,14 @@ def main():
         # the metric's "achieved HBM GB/s vs peak", for the hidden-layer forward
         # GEMM (the north star's fused LCN forward): algorithmic bytes = read the
         # input activations + write z, 2 x 17*F floats per pose
+        hbm_ew = None
+        nba, msba, bytes_ba = bn_act_timing
+        if nba:
+            gbs = bytes_ba / (msba * 1e-3) / 1e9
+            hbm_ew = {"kernel": "bn_act (BN apply + LeakyReLU + residual add, materialising the block "
+                                "outputs of the fused forward)", "launches": nba,
+                      "avg_ms": round(msba / nba, 4), "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
         hbm = None
         if "gemm_fwd" in kern:
             f = kern["gemm_fwd"]
@@ -288,6 +297,7 @@ def main():
                        "channels": args.channels, "parallelism": f"dp{world} (SyncBN + RCCL grad all-reduce)"},
             "roofline": roof,
             "hbm": hbm,
+            "hbm_elementwise": hbm_ew,
             "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv for kk, vv in v.items()}
                         for k, v in kern.items()},
             "fwd_only_poses_per_s": round(B * world * nf / tfwd, 1),

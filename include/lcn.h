@@ -197,7 +197,9 @@ uint32_t lcn_crc32c(uint32_t crc, const void* data, int64_t n);
 
 /* --- instrumentation --------------------------------------------------- */
 /* kernel ids for lcn_kernel_timing */
-enum { LCN_K_GEMM_FWD = 0, LCN_K_GEMM_DX = 1, LCN_K_GEMM_DW = 2, LCN_K_NUM = 3 };
+/* LCN_K_BN_ACT: the BN apply + LeakyReLU (+ residual) pass that materialises
+ * the block outputs; its "flops" field accumulates algorithmic HBM bytes */
+enum { LCN_K_GEMM_FWD = 0, LCN_K_GEMM_DX = 1, LCN_K_GEMM_DW = 2, LCN_K_BN_ACT = 3, LCN_K_NUM = 4 };
 int lcn_set_timing(void* handle, int32_t enable);
 int lcn_kernel_timing(void* handle, int32_t kernel, int64_t* launches, double* total_ms,
                       double* flops);

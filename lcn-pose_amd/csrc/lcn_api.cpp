@@ -711,6 +711,16 @@ int bn_back(Handle* h, int k, int B) {
   return LCN_OK;
 }
 
+// BN apply + LeakyReLU (+ residual, + dropout) of BN layer k into a block
+// output, timed as LCN_K_BN_ACT with its algorithmic HBM bytes
+void bn_act_timed(Handle* h, const float* z, const float* res, float* out, int k, int B) {
+  hipEvent_t ev[2];
+  tstart(h, LCN_K_BN_ACT, ev);
+  launch_bn_act(z, res, out, h->bn[k].scale, h->bn[k].shift, h->F, h->alpha, B, h->nslab,
+                drop_of(h, k, B), h->stream);
+  tstop(h, LCN_K_BN_ACT, ev, (res ? 3.0 : 2.0) * 4.0 * (double)B * h->H);
+}
+
 int forward(Handle* h, int B, bool with_labels, bool train) {
   hipStream_t s = h->stream;
   const int S = h->nslab, nl = h->nl;
@@ -723,8 +733,7 @@ int forward(Handle* h, int B, bool with_labels, bool train) {
   CHECK(gemm(h, GemmCall{raw(h->x, 1), h->wl[0].blk_fwd, h->thin_ptr, h->thin_idx, S,
                          h->theta + h->b_off[0], h->Z[0], S, nullptr, epi, -1, -1, thin_flops}, B));
   CHECK(bn_stats(h, 0, B));
-  launch_bn_act(h->Z[0], nullptr, h->Hb[0], h->bn[0].scale, h->bn[0].shift, h->F, h->alpha, B, S,
-                drop_of(h, 0, B), s);
+  bn_act_timed(h, h->Z[0], nullptr, h->Hb[0], 0, B);
   // two_linear blocks (models_att.py:630-705)
   for (int l = 0; l < h->L; ++l) {
     const int k1 = 2 * l + 1, k2 = 2 * l + 2;
@@ -740,8 +749,7 @@ int forward(Handle* h, int B, bool with_labels, bool train) {
     }
     CHECK(gemm_hidden(h, k2, LCN_K_GEMM_FWD, g, h->Z[k2], nullptr, epi, -1, B));
     CHECK(bn_stats(h, k2, B));
-    launch_bn_act(h->Z[k2], h->residual ? h->Hb[l] : nullptr, h->Hb[l + 1], h->bn[k2].scale,
-                  h->bn[k2].shift, h->F, h->alpha, B, S, drop_of(h, k2, B), s);
+    bn_act_timed(h, h->Z[k2], h->residual ? h->Hb[l] : nullptr, h->Hb[l + 1], k2, B);
   }
   // output layer y = h_L . W4e + b4 into a 1-slab buffer (51 used), then the
   // output assembly, loss and d out (models_att.py:749-773, :356)

@@ -35,6 +35,8 @@ def test_train_line_has_the_contract_keys():
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
     assert 0 < d["hbm"]["frac"] < 1
+    ew = d["hbm_elementwise"]
+    assert ew["launches"] == 3 * 4 and 0 < ew["frac"] < 1   # lift + 3 blocks per step
 
 
 def test_predict_mode():
