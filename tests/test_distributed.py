@@ -5,7 +5,7 @@ layer -> RCCL all-reduce (float64) -> SyncBN statistics; per-rank BN-backward
 sums -> all-reduce -> dz coefficients; LOCAL raw gradients (dW_e, db, dgamma,
 dbeta with the global-batch loss scale) -> one all-reduce of the raw-gradient
 vector -> mask / clip backward, regularisation and Adam on every rank
-(lcn-pose_amd/csrc/lcn_api.cpp bn_stats, bn_back, finish_and_update).
+(lcn-pose_amd/csrc/lcn_api.cpp bn_stats, bn_back, finish_device).
 
 oracle.sharded_grads restates exactly that decomposition; these tests run it on
 2 and 3 gloo ranks with uneven, ragged shards and check it reproduces the
