@@ -36,6 +36,25 @@ HBM_PEAK_GBS = 8000.0
 METRIC = "poses/sec (17-joint LCN fwd+bwd) at 1/2/4/8 GPU; achieved HBM GB/s vs peak"
 
 
+def _claim_stdout():
+    """Keep stdout for the one JSON line: RCCL prints its version banner to
+    stdout from ncclCommInitRank on rank 0, so everything the native side (or
+    anything else) writes to fd 1 goes to stderr and the result line is
+    written to a private duplicate of the original stdout."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
+
+
+RESULT_OUT = sys.stdout
+
+
+def emit(res: dict):
+    RESULT_OUT.write(json.dumps(res) + "\n")
+    RESULT_OUT.flush()
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -46,6 +65,9 @@ def parse():
     ap.add_argument("--layers", type=int, default=3)
     ap.add_argument("--channels", type=int, default=64)
     ap.add_argument("--mask-type", default="locally_connected")
+    ap.add_argument("--rccl-self", type=int, default=0,
+                    help="at N=1, create a one-rank RCCL communicator so the step runs the "
+                         "multi-GPU path (phased SyncBN, RCCL all-reduces)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic.json"))
@@ -125,7 +147,7 @@ def predict_main(args, rank, world, local):
     mask = (neighbour.T != 0).astype(np.float32)
     net = native.Network(F=args.channels, in_F=2, num_layers=args.layers, mask_type=args.mask_type,
                          mask_matrix=mask, max_batch=B, device=local)
-    if world > 1:
+    if world > 1 or args.rccl_self:
         net.comm_init(exchange_uid(rank, world), rank, world)
     net.set_params(init_flat(net.param_layout(), net.n_params, neighbour, seed=0))
     rng = np.random.default_rng(99 + rank)
@@ -142,7 +164,7 @@ def predict_main(args, rank, world, local):
     net.allreduce_host([0.0])
     el = float(net.allreduce_host([time.perf_counter() - t0], op="max")[0])
     if rank == 0:
-        print(json.dumps({
+        emit({
             "metric": "poses/sec, TTA predict (flip + rotation, 3 copies per pose)",
             "value": round(B * world * args.steps / el, 1), "unit": "poses/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
@@ -152,12 +174,14 @@ def predict_main(args, rank, world, local):
                                    f"layers={args.layers}, F={args.channels}, flip+rotation TTA",
                        "poses_per_gpu": B, "network_batch": B, "copies": 3,
                        "parallelism": f"dp{world} (SyncBN over the ranks' batches)"},
-            "finite": bool(np.isfinite(pred).all())}), flush=True)
+            "finite": bool(np.isfinite(pred).all())})
     net.close()
 
 
 def main():
+    global RESULT_OUT
     args = parse()
+    RESULT_OUT = _claim_stdout()
     if args.mode == "predict":
         rank, world, local = dist_env()
         return predict_main(args, rank, world, local)
@@ -175,7 +199,7 @@ def main():
         mask = get_exponential_matrix(verbose=False)
     net = native.Network(F=args.channels, in_F=2, num_layers=args.layers, mask_type=args.mask_type,
                          mask_matrix=mask, max_batch=B, device=local)
-    if world > 1:
+    if world > 1 or args.rccl_self:
         net.comm_init(exchange_uid(rank, world), rank, world)
     net.set_params(init_flat(net.param_layout(), net.n_params, neighbour, seed=0))
 
@@ -294,7 +318,8 @@ def main():
             "config": {"workload": "cfg3: H36M 17-joint LCN train step (fwd+bwd+Adam), "
                                    f"{args.mask_type} knn={args.knn}",
                        "global_batch": B * world, "per_gpu_batch": B, "layers": args.layers,
-                       "channels": args.channels, "parallelism": f"dp{world} (SyncBN + RCCL grad all-reduce)"},
+                       "channels": args.channels, "parallelism": f"dp{world} (SyncBN + RCCL grad all-reduce)"
+                       + (", one-rank RCCL communicator" if world == 1 and args.rccl_self else "")},
             "roofline": roof,
             "hbm": hbm,
             "hbm_elementwise": hbm_ew,
@@ -307,7 +332,7 @@ def main():
             res["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
         else:
             res["cpu_baseline"] = None
-        print(json.dumps(res), flush=True)
+        emit(res)
     net.close()
 
 

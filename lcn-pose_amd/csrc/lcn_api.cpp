@@ -6,7 +6,7 @@
 //   backward (optimizer.compute_gradients, :408) + Adam (:404-409)
 //
 // One HIP stream per handle; every launch is stream-ordered, the host only
-// synchronises when a result is copied back.  With world > 1 (one process per
+// synchronises when a result is copied back.  After lcn_comm_init (one process per
 // GPU) the data-parallel exchanges are RCCL all-reduces on the same stream:
 // SyncBN statistics (the reference BN always uses whole-batch statistics) and
 // one all-reduce of the raw gradient vector per step.
@@ -138,8 +138,9 @@ struct Handle {
   // communication
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
-  // run the multi-GPU (phase 1 -> all-reduce -> phase 2) BN reductions even
-  // with world == 1 (LCN_FORCE_PHASED=1 at create): lets one GPU test that path
+  // run the multi-GPU (phase 1 -> all-reduce -> phase 2) BN reductions without
+  // a communicator (LCN_FORCE_PHASED=1 at create); with one (lcn_comm_init,
+  // any world size) they always run phased
   bool phased = false;
 
 
@@ -490,7 +491,7 @@ int build(Handle* h, const lcn_config* c) {
 // step pieces
 // ---------------------------------------------------------------------------
 int allreduce(Handle* h, void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op = ncclSum) {
-  if (h->world <= 1) return LCN_OK;
+  if (!h->comm) return LCN_OK;
   NCCLC(ncclAllReduce(buf, buf, count, dt, op, h->comm, h->stream));
   return LCN_OK;
 }
@@ -544,7 +545,7 @@ int bn_stats(Handle* h, int k, int B) {
   const float* gamma = h->theta + h->gamma_off[k];
   const float* beta = h->theta + h->beta_off[k];
   launch_colreduce(h->stat_part, (int)cdiv(B, kGemmRows), kGemmRows, B, h->H, 1, h->colacc, s);
-  if (!h->phased && h->world == 1) {
+  if (!h->phased && !h->comm) {
     launch_bn_fwd_finalize(h->colacc, h->H, h->F, 0, count, gamma, beta, h->eps, h->acc1, h->bn[k],
                            h->zsum[k], s);
     return LCN_OK;
@@ -698,7 +699,7 @@ int bn_back(Handle* h, int k, int B) {
   float* dbet = bn ? h->rg + h->beta_off[k] : nullptr;
   float* db = h->rg + h->b_off[k];
   launch_colreduce(h->stat_part, (int)cdiv(B, kGemmRows), kGemmRows, B, h->H, 0, h->colacc, s);
-  if ((!h->phased && h->world == 1) || !bn) {
+  if ((!h->phased && !h->comm) || !bn) {
     launch_bn_bwd_finalize(h->colacc, h->H, h->F, 0, bn, count, (double)B, gamma, st.mean, st.rstd,
                            h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
     return LCN_OK;
@@ -819,7 +820,7 @@ int backward(Handle* h, int B) {
 // the device side of the update: mask / clip backward, Adam (lr_t from lr_dev)
 int finish_device(Handle* h, bool update, bool keep_grads) {
   hipStream_t s = h->stream;
-  if (h->world > 1) {
+  if (h->comm) {
     CHECK(allreduce(h, h->rg, (size_t)h->P, ncclFloat));
   }
   launch_wdot(h->rg, h->theta, h->w_offs, h->w_kin, h->w_nout, h->nl, h->blocksum, s);
@@ -1047,7 +1048,7 @@ int lcn_forward_loss(void* handle, const float* x, const float* labels, float* o
   HIPC(hipSetDevice(h->device));
   CHECK(stage_inputs(h, x, labels, B, flags));
   CHECK(forward(h, (int)B, true, false));
-  if (h->world > 1) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
+  if (h->comm) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
   CHECK(finish_launches(h));
   CHECK(copy_out(h, out, B, flags));
   CHECK(read_loss(h, B, loss));
@@ -1058,7 +1059,7 @@ int lcn_forward_loss(void* handle, const float* x, const float* labels, float* o
 // forward, loss, backward and update of one step, enqueued on the stream
 static int enqueue_step(Handle* h, int64_t B, bool update, bool keep) {
   CHECK(forward(h, (int)B, true, true));
-  if (h->world > 1) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
+  if (h->comm) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
   CHECK(backward(h, (int)B));
   return finish_device(h, update, keep);
 }
@@ -1093,7 +1094,7 @@ static int run_train_step(Handle* h, int64_t B, int32_t flags, float* loss_out, 
   std::memcpy(&lr_bits, &lr_t, 4);
   HIPC(hipMemsetD32Async((hipDeviceptr_t)h->lr_dev, (int)lr_bits, 1, h->stream));
   hipGraphExec_t exec = nullptr;
-  if (h->use_graphs && h->world == 1 && !h->timing && h->drop_rate == 0.f &&
+  if (h->use_graphs && !h->comm && !h->timing && h->drop_rate == 0.f &&
       step_graph(h, B, update, keep, &exec) != LCN_OK) {
     // capture unavailable: fall back to direct launches for this handle
     std::fprintf(stderr, "liblcn: step graph disabled (%s)\n", h->err.c_str());
@@ -1252,7 +1253,7 @@ int lcn_predict_dataset(void* handle, int32_t x_slot, int32_t lab_slot, int64_t 
   }
   const int64_t N = dx->rows, total = N * a.n_copies;
   int64_t nb = cdiv(total, batch_size);
-  if (h->world > 1) {  // every rank runs the same number of (SyncBN) batches
+  if (h->comm) {  // every rank runs the same number of (SyncBN) batches
     double v = (double)nb;
     CHECK(lcn_comm_allreduce_host(h, &v, 1, 1));
     nb = (int64_t)v;
@@ -1290,7 +1291,7 @@ int lcn_predict_dataset(void* handle, int32_t x_slot, int32_t lab_slot, int64_t 
     CHECK(gather_batch(h, dx, dl, nullptr, begin, a, batch_size));
     CHECK(forward(h, (int)batch_size, dl != nullptr, false));
     if (dl) {
-      if (h->world > 1) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
+      if (h->comm) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
       launch_batch_loss(h->loss_sum, (double)batch_size * h->world * 51.0, h->batch_losses, (int)i,
                         h->stream);
     }
@@ -1373,8 +1374,11 @@ int lcn_comm_unique_id(void* id_out) {
 int lcn_comm_init(void* handle, const void* id_in, int32_t rank, int32_t world) {
   Handle* h = (Handle*)handle;
   if (!h || !id_in || world < 1 || rank < 0 || rank >= world) return LCN_E_ARG;
+  if (h->comm) { h->err = "lcn_comm_init: the handle already has a communicator"; return LCN_E_ARG; }
   HIPC(hipSetDevice(h->device));
-  if (world == 1) { h->rank = 0; h->world = 1; return LCN_OK; }
+  // a real communicator even at world 1: every exchange below is gated on
+  // h->comm, so a one-GPU run after comm_init takes the multi-GPU code path
+  // (phased BN reductions, RCCL all-reduces) end to end
   ncclUniqueId id;
   std::memcpy(&id, id_in, sizeof(id));
   NCCLC(ncclCommInitRank(&h->comm, world, id, rank));
@@ -1386,7 +1390,7 @@ int lcn_comm_init(void* handle, const void* id_in, int32_t rank, int32_t world) 
 int lcn_comm_allreduce_host(void* handle, double* values, int32_t count, int32_t op) {
   Handle* h = (Handle*)handle;
   if (!h || !values || count <= 0 || count > 2 * h->F) return LCN_E_ARG;
-  if (h->world == 1) return LCN_OK;
+  if (!h->comm) return LCN_OK;
   HIPC(hipSetDevice(h->device));
   HIPC(hipStreamSynchronize(h->stream));
   HIPC(hipMemcpy(h->acc2, values, count * sizeof(double), hipMemcpyHostToDevice));

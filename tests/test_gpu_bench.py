@@ -42,3 +42,14 @@ def test_train_line_has_the_contract_keys():
 def test_predict_mode():
     d = _bench("--mode", "predict", "--knn", "5", "--batch", "4096", "--steps", "2", "--warmup", "1")
     assert d["value"] > 0 and d["finite"] and d["config"]["copies"] == 3
+
+
+def test_train_line_with_an_rccl_communicator_is_alone_on_stdout():
+    """With a communicator (one rank here; every rank at N > 1) RCCL prints
+    its version banner to stdout on rank 0; bench.py must still print only
+    the JSON line there."""
+    d = _bench("--batch", "4096", "--steps", "2", "--warmup", "1", "--cpu-baseline", "0",
+               "--rccl-self", "1")
+    assert d["value"] > 0 and "one-rank RCCL" in d["config"]["parallelism"]
+    d = _bench("--mode", "predict", "--batch", "2048", "--steps", "1", "--warmup", "1", "--rccl-self", "1")
+    assert d["value"] > 0 and d["finite"]

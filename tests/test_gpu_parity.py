@@ -143,6 +143,35 @@ def test_phased_reductions_match_single_pass(monkeypatch):
         assert rel_err(g1[off:off + n], g0[off:off + n]) < 1e-6, name
 
 
+def test_single_rank_rccl_communicator_runs_the_multi_gpu_path(monkeypatch):
+    """lcn_comm_init with world 1 creates a real RCCL communicator, so every
+    data-parallel exchange of the multi-GPU path runs on one GPU: the phased
+    SyncBN reductions with their ncclAllReduce (float64), the gradient
+    all-reduce (float32) before Adam and the loss all-reduce, plus the host
+    all-reduce bench.py uses as a barrier.  A sum over one rank is the
+    identity, so two Adam steps and a forward must equal, bit for bit, the
+    same steps on the phased path without a communicator."""
+    from lcn_amd.native import LcnNativeError, Network
+    cfg, params, x, lab, net = _setup(dict(F=64, L=2, knn=3), 300)
+    monkeypatch.setenv("LCN_FORCE_PHASED", "1")
+    ref = make_network(cfg, max_batch=300)
+    monkeypatch.delenv("LCN_FORCE_PHASED")
+    ref.set_params(O.flatten(cfg, params))
+    net.comm_init(Network.comm_unique_id(), 0, 1)
+    losses = []
+    for n in (ref, net):
+        l1, _ = n.train_step(x, lab)
+        l2, _ = n.train_step(x[::-1].copy(), lab[::-1].copy())
+        losses.append((l1, l2))
+    assert losses[0] == losses[1]
+    assert np.array_equal(net.get_params(), ref.get_params())
+    assert np.array_equal(net.forward(x), ref.forward(x))
+    assert list(net.allreduce_host([1.5, -2.0])) == [1.5, -2.0]
+    assert list(net.allreduce_host([3.0], op="max")) == [3.0]
+    with pytest.raises(LcnNativeError):
+        net.comm_init(Network.comm_unique_id(), 0, 1)
+
+
 def test_full_size_cfg3_matches_oracle():
     """BASELINE.json configs[1] at its full size (B = 65 536, F = 64, L = 3,
     knn = 3): outputs and every gradient against the float64 oracle."""
