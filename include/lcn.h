@@ -168,6 +168,14 @@ int lcn_predict_dataset(void* handle, int32_t x_slot, int32_t lab_slot, int64_t 
                         float* batch_losses, int64_t losses_cap, int64_t* n_batches);
 
 /* --- data parallel (RCCL over xGMI) ------------------------------------ */
+/* Replaces the single-process Session of models_att.py:155, 210-212 with one
+ * process per GPU.  lcn_comm_init creates an RCCL communicator at any world
+ * size (world 1 included: the multi-GPU path then runs on one GPU) and may be
+ * called once per handle (LCN_E_ARG otherwise).  After it, every step does
+ * SyncBN (phased BN reductions + ncclAllReduce, float64) and one float32
+ * all-reduce of the raw gradient vector on the handle's stream.
+ * lcn_comm_allreduce_host: count <= 2F doubles, a no-op without a
+ * communicator. */
 int lcn_comm_unique_id(void* id_out /* 128 bytes */);
 int lcn_comm_init(void* handle, const void* id /* 128 bytes */, int32_t rank, int32_t world);
 int lcn_comm_allreduce_host(void* handle, double* values, int32_t count, int32_t op /* 0 sum, 1 max */);
