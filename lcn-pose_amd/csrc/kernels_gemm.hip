@@ -206,25 +206,43 @@ void launch_gemm_dw(const GemmDwArgs& a, hipStream_t s) {
 // Sum the chunk partials of every block in a fixed order and scatter into the
 // dense gradient dW[rows][ld]; rows / columns past (rows_valid, cols_valid)
 // are the zero padding of the thin lift / output layers and are dropped.
+// Each thread owns 4 adjacent columns (float4 loads) and keeps 8 chunk loads
+// in flight; the additions stay in chunk order c = 0, 1, ... (deterministic,
+// the same sums as a plain sequential loop).
 __global__ __launch_bounds__(256) void dw_reduce_kernel(const float* __restrict__ part, int nchunks,
                                                         int nblk, const int2* __restrict__ blk,
                                                         float* __restrict__ dW, int ld,
                                                         int rows_valid, int cols_valid) {
   const int b = blockIdx.y;
-  const int e = blockIdx.x * 256 + threadIdx.x;  // 0..4095
+  const int e = (blockIdx.x * 256 + threadIdx.x) * 4;  // 0..4092
   const int2 sb = blk[b];
   const int row = sb.x * kSlab + (e >> 6), col = sb.y * kSlab + (e & 63);
   if (row >= rows_valid || col >= cols_valid) return;
-  const size_t stride = (size_t)nblk * 4096;
-  const float* p = part + (size_t)b * 4096 + e;
-  float s = 0.f;
-  for (int c = 0; c < nchunks; ++c) s += p[c * stride];
-  dW[(size_t)row * ld + col] = s;
+  const size_t stride4 = (size_t)nblk * 1024;
+  const float4* p = (const float4*)(part + (size_t)b * 4096 + e);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  int c = 0;
+  for (; c + 8 <= nchunks; c += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = p[(size_t)(c + k) * stride4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s.x += v[k].x; s.y += v[k].y; s.z += v[k].z; s.w += v[k].w; }
+  }
+  for (; c < nchunks; ++c) {
+    const float4 v = p[(size_t)c * stride4];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  float* o = dW + (size_t)row * ld + col;
+  const float sv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (col + k < cols_valid) o[k] = sv[k];
 }
 
 void launch_dw_reduce(const float* part, int nchunks, int nblk, const int2* blk, float* dW, int ld,
                       int rows_valid, int cols_valid, hipStream_t s) {
-  hipLaunchKernelGGL(dw_reduce_kernel, dim3(16, nblk), dim3(256), 0, s, part, nchunks, nblk, blk,
+  hipLaunchKernelGGL(dw_reduce_kernel, dim3(4, nblk), dim3(256), 0, s, part, nchunks, nblk, blk,
                      dW, ld, rows_valid, cols_valid);
 }
 

@@ -226,7 +226,8 @@ int upload_dw_groups(Handle* h, const std::vector<int2>& blk, int4** dev, int* n
 // LCN_DW_ROWS overrides the block-rows budget (tuning runs)
 int dw_chunks(int nblk) {
   static const int budget = std::getenv("LCN_DW_ROWS") ? std::atoi(std::getenv("LCN_DW_ROWS")) : 5600;
-  return std::max(1, std::min(64, budget / std::max(1, nblk)));
+  static const int cap = std::getenv("LCN_DW_MAXCH") ? std::atoi(std::getenv("LCN_DW_MAXCH")) : 64;
+  return std::max(1, std::min(cap, budget / std::max(1, nblk)));
 }
 
 // ---------------------------------------------------------------------------
