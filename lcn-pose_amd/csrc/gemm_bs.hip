@@ -243,13 +243,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
 #pragma unroll
     for (int q = 0; q < 8; ++q) put(q, v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
     __syncthreads();
-    float sum = 0.f;
-    for (int r = 0; r < n; ++r) sum += get(r);
-    const float mean = n > 0 ? sum / (float)n : 0.f;
-    float m2 = 0.f;
-    for (int r = 0; r < n; ++r) {
-      const float d = get(r) - mean;
-      m2 = fmaf(d, d, m2);
+    float sum = 0.f, mean = 0.f, m2 = 0.f;
+    if (n == kRT) {  // full tile: 16 reads in flight at a time; / 32 is exact as * (1/32)
+#pragma unroll
+      for (int r0 = 0; r0 < kRT; r0 += 16) {
+        float col[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) col[r] = get(r0 + r);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sum += col[r];
+      }
+      mean = sum * (1.f / kRT);
+#pragma unroll
+      for (int r0 = 0; r0 < kRT; r0 += 16) {
+        float col[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) col[r] = get(r0 + r);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float d = col[r] - mean;
+          m2 = fmaf(d, d, m2);
+        }
+      }
+    } else {
+      for (int r = 0; r < n; ++r) sum += get(r);
+      mean = n > 0 ? sum / (float)n : 0.f;
+      for (int r = 0; r < n; ++r) {
+        const float d = get(r) - mean;
+        m2 = fmaf(d, d, m2);
+      }
     }
     comb[(w * 64 + c) * 3 + 0] = sum;
     comb[(w * 64 + c) * 3 + 1] = m2;
@@ -299,7 +321,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
       put(q, v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);                          \
     }                                                                                      \
     __syncthreads();                                                                       \
-    for (int r = 0; r < n; ++r) P_ += get(r);                                              \
+    P_ = colsum(n);                                                                        \
     __syncthreads();                                                                       \
     _Pragma("unroll") for (int q = 0; q < 8; ++q) {                                        \
       const float4 z4 = zq[q];                                                             \
@@ -309,8 +331,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
           v[4 * q + 2] * ((z4.z - mu.z) * rs.z), v[4 * q + 3] * ((z4.w - mu.w) * rs.w));   \
     }                                                                                      \
     __syncthreads();                                                                       \
-    for (int r = 0; r < n; ++r) Q_ += get(r);                                              \
+    Q_ = colsum(n);                                                                        \
   }
+  // column c summed over the tile's n rows in row order (a full tile with
+  // 16 LDS reads in flight at a time)
+  auto colsum = [&](int nr) {
+    float acc = 0.f;
+    if (nr == kRT) {
+#pragma unroll
+      for (int r0 = 0; r0 < kRT; r0 += 16) {
+        float col[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) col[r] = get(r0 + r);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc += col[r];
+      }
+    } else {
+      for (int r = 0; r < nr; ++r) acc += get(r);
+    }
+    return acc;
+  };
   float P_ = 0.f, Q_ = 0.f;
   BNBACK_EPI(zp)
 #undef BNBACK_EPI
