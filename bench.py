@@ -85,11 +85,28 @@ def dist_env():
     return rank, world, local
 
 
-def exchange_uid(rank, world):
-    """rank 0 publishes the RCCL unique id in a file every rank on the node can read."""
+def _uid_path():
     key = "_".join([os.environ.get("MASTER_ADDR", "127.0.0.1"), os.environ.get("MASTER_PORT", "0"),
                     os.environ.get("TORCHELASTIC_RUN_ID", "x"), str(os.getppid())])
-    path = os.path.join("/tmp", f"lcn_rccl_uid_{key}.bin")
+    return os.path.join("/tmp", f"lcn_rccl_uid_{key}.bin")
+
+
+def comm_setup(net, rank, world):
+    """RCCL communicator over the node's ranks; once every rank holds it (the
+    host all-reduce below is its first collective) rank 0 removes the id
+    file, so a later launch can never read a stale id."""
+    net.comm_init(exchange_uid(rank, world), rank, world)
+    net.allreduce_host([0.0])
+    if rank == 0:
+        try:
+            os.remove(_uid_path())
+        except OSError:
+            pass
+
+
+def exchange_uid(rank, world):
+    """rank 0 publishes the RCCL unique id in a file every rank on the node can read."""
+    path = _uid_path()
     if rank == 0:
         uid = native.Network.comm_unique_id()
         tmp = path + ".tmp"
@@ -148,7 +165,7 @@ def predict_main(args, rank, world, local):
     net = native.Network(F=args.channels, in_F=2, num_layers=args.layers, mask_type=args.mask_type,
                          mask_matrix=mask, max_batch=B, device=local)
     if world > 1 or args.rccl_self:
-        net.comm_init(exchange_uid(rank, world), rank, world)
+        comm_setup(net, rank, world)
     net.set_params(init_flat(net.param_layout(), net.n_params, neighbour, seed=0))
     rng = np.random.default_rng(99 + rank)
     x = rng.uniform(-1, 1, (B, 34))                      # float64, as DataReader yields
@@ -200,7 +217,7 @@ def main():
     net = native.Network(F=args.channels, in_F=2, num_layers=args.layers, mask_type=args.mask_type,
                          mask_matrix=mask, max_batch=B, device=local)
     if world > 1 or args.rccl_self:
-        net.comm_init(exchange_uid(rank, world), rank, world)
+        comm_setup(net, rank, world)
     net.set_params(init_flat(net.param_layout(), net.n_params, neighbour, seed=0))
 
     # synthetic poses resident in HBM (x ~ U(-1,1); labels = lifted x + noise)
