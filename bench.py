@@ -2,22 +2,30 @@
 backward + Adam) on synthetic data resident in HBM.
 
 Workload (BASELINE.json configs[2], "cfg3"): H36M 17-joint, locally
-connected mask, knn=3, layers=3, F=64, batch 65 536 poses per GPU (weak
-scaling: the global batch is 65 536 x N with SyncBN over all of it).
+connected mask, knn=3, layers=3, F=64, GLOBAL batch 65 536 poses per step.
+With N GPUs the batch is sharded (rank r takes rows r*G/N ..., SyncBN over
+all of it, one RCCL all-reduce of the gradients): strong scaling, the same
+model step at every N.  `--batch b` instead keeps b poses per GPU (weak
+scaling, global batch b*N -- a different BN batch, hence a different step).
+`--config cfg4|cfg5` select BASELINE.json configs[3] / configs[4].
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-One process per GPU; ranks find each other through RCCL (librccl, bootstrapped
-with a unique id passed through a file on the node).  No torch import: the
-product path is liblcn.so through ctypes.  Rank 0 prints ONE JSON line.
+One process per GPU.  Under torch.distributed.run the ranks come from
+RANK / LOCAL_RANK / WORLD_SIZE; run plainly with --gpus N > 1, this process
+(which never touches the GPU) starts the N ranks itself and fails if any of
+them does.  Ranks find each other through RCCL (librccl, bootstrapped with a
+unique id passed through a file on the node).  No torch import: the product
+path is liblcn.so through ctypes.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,7 +34,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "lcn-pose_amd"))
 
-from lcn_amd import native  # noqa: E402
+from lcn_amd import dist, native  # noqa: E402
 from lcn_amd.init import init_flat  # noqa: E402
 from tools.params_help import get_neighbour_matrix_by_hand  # noqa: E402
 from tools.filter_hub import neighbour_dict_set  # noqa: E402
@@ -56,103 +64,177 @@ def emit(res: dict):
     RESULT_OUT.flush()
 
 
-def parse():
+# BASELINE.json configs[2..4]: model shape, global batch, bench mode
+CONFIGS = {
+    "cfg3": dict(knn=3, layers=3, channels=64, mask_type="locally_connected", global_batch=65536,
+                 mode="train"),
+    "cfg4": dict(knn=2, layers=6, channels=256, mask_type="exponential", global_batch=131072,
+                 mode="train"),
+    "cfg5": dict(knn=5, layers=3, channels=64, mask_type="locally_connected", global_batch=262144,
+                 mode="predict"),
+}
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=65536, help="poses per GPU per step")
-    ap.add_argument("--knn", type=int, default=3)
-    ap.add_argument("--layers", type=int, default=3)
-    ap.add_argument("--channels", type=int, default=64)
-    ap.add_argument("--mask-type", default="locally_connected")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg3",
+                    help="BASELINE.json config: model shape, global batch and mode defaults")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="poses per step over all GPUs, sharded across them (strong scaling; "
+                         "default: the config's)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="poses per GPU per step (weak scaling: global batch = batch x GPUs)")
+    ap.add_argument("--knn", type=int, default=None)
+    ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--channels", type=int, default=None)
+    ap.add_argument("--mask-type", default=None)
     ap.add_argument("--rccl-self", type=int, default=0,
                     help="at N=1, create a one-rank RCCL communicator so the step runs the "
                          "multi-GPU path (phased SyncBN, RCCL all-reduces)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic.json"))
-    ap.add_argument("--mode", choices=["train", "predict"], default="train",
+    ap.add_argument("--mode", choices=["train", "predict"], default=None,
                     help="train: the headline training step (default); predict: cfg5-style "
                          "inference -- float64 poses resident in HBM, flip + rotation TTA "
                          "(3 copies), batch-statistics BN, undo + average on the device")
-    return ap.parse_args()
+    args = ap.parse_args(argv)
+    preset = CONFIGS[args.config]
+    for k in ("knn", "layers", "channels", "mask_type", "mode"):
+        if getattr(args, k) is None:
+            setattr(args, k, preset[k])
+    if args.batch is not None and args.global_batch is not None:
+        ap.error("--batch (per GPU, weak scaling) and --global-batch (sharded, strong scaling) exclude each other")
+    if args.batch is None and args.global_batch is None:
+        args.global_batch = preset["global_batch"]
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    return args
 
 
-def dist_env():
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    return rank, world, local
+dist_env = dist.dist_env
+shard_rows = dist.shard_rows
 
 
-def _uid_path():
-    key = "_".join([os.environ.get("MASTER_ADDR", "127.0.0.1"), os.environ.get("MASTER_PORT", "0"),
-                    os.environ.get("TORCHELASTIC_RUN_ID", "x"), str(os.getppid())])
-    return os.path.join("/tmp", f"lcn_rccl_uid_{key}.bin")
+def batch_plan(args, world, rank):
+    """(rows of this rank, global rows, scaling label)."""
+    if args.batch is not None:
+        return args.batch, args.batch * world, "weak"
+    if args.global_batch < world:
+        raise SystemExit(f"--global-batch {args.global_batch} < {world} ranks")
+    return shard_rows(args.global_batch, world, rank), args.global_batch, "strong"
 
 
-def comm_setup(net, rank, world):
-    """RCCL communicator over the node's ranks; once every rank holds it (the
-    host all-reduce below is its first collective) rank 0 removes the id
-    file, so a later launch can never read a stale id."""
-    net.comm_init(exchange_uid(rank, world), rank, world)
-    net.allreduce_host([0.0])
-    if rank == 0:
-        try:
-            os.remove(_uid_path())
-        except OSError:
-            pass
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
-def exchange_uid(rank, world):
-    """rank 0 publishes the RCCL unique id in a file every rank on the node can read."""
-    path = _uid_path()
-    if rank == 0:
-        uid = native.Network.comm_unique_id()
-        tmp = path + ".tmp"
-        with open(tmp, "wb") as f:
-            f.write(uid)
-        os.replace(tmp, path)
-        return uid
-    t0 = time.time()
-    while not os.path.exists(path):
-        if time.time() - t0 > 300:
-            raise RuntimeError("timed out waiting for the RCCL unique id")
+def spawn_ranks(args, argv, script=None):
+    """`bench.py --gpus N` run plainly: start the N ranks as child processes
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, stdout
+    inherited so rank 0's JSON line is this command's), wait for all of them,
+    and fail if any fails.  This process makes no GPU call."""
+    port = str(_free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__), *argv],
+                                      env=env))
+    codes = [None] * len(procs)
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+        failed = [i for i, c in enumerate(codes) if c not in (None, 0)]
+        if failed:  # a rank died: the others would wait in a collective for ever
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    try:
+                        codes[i] = p.wait(timeout=20)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        codes[i] = p.wait()
+            print(f"bench.py: rank(s) {failed} failed with exit code(s) "
+                  f"{[codes[i] for i in failed]}", file=sys.stderr)
+            return 1
         time.sleep(0.05)
-    time.sleep(0.05)
-    with open(path, "rb") as f:
-        return f.read()
+    return 0
 
 
-def cpu_baseline(args, seconds):
-    """The numpy restatement (oracle/lcn_oracle.py) timed on this host's cores:
-    a bounded sample of the same training step (float32, smaller batch)."""
+# the RCCL bootstrap lives with the product (cgcnn uses it too)
+_uid_path = dist.uid_path
+exchange_uid = dist.exchange_uid
+comm_setup = dist.comm_setup
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _blas_name():
+    try:
+        cfg = np.show_config(mode="dicts")
+        b = cfg.get("Build Dependencies", {}).get("blas", {})
+        return f"{b.get('name', 'unknown')} {b.get('version', '')}".strip()
+    except Exception:  # noqa: BLE001
+        return "unknown"
+
+
+def cpu_baseline(args, seconds, batches=(256, 4096, 65536)):
+    """The numpy restatement (oracle/lcn_oracle.py) of the same training step
+    (float32, forward + backward + Adam) timed on this host's cores: at cfg1's
+    batch 256, at 4 096, and at the headline batch 65 536.  `seconds` bounds
+    the whole leg (each size gets a third; a size whose first step already
+    exceeds what is left is skipped).  `value` is the largest batch timed."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import lcn_oracle as O
     cfg = O.Config(F=args.channels, num_layers=args.layers, mask_type=args.mask_type,
                    neighbour=O.neighbour_matrix(args.knn))
     params = O.init_params(cfg, seed=0)
     st = O.adam_init(cfg, params)
-    B = 4096
-    rng = np.random.default_rng(0)
-    x = rng.uniform(-1, 1, (B, 34)).astype(np.float32)
-    lab = rng.uniform(-1, 1, (B, 51)).astype(np.float32)
-    O.train_step(cfg, params, st, x, lab)  # warm-up
-    times = []
-    t_end = time.time() + seconds
-    while time.time() < t_end or len(times) < 3:
-        t0 = time.perf_counter()
-        O.train_step(cfg, params, st, x, lab)
-        times.append(time.perf_counter() - t0)
-        if len(times) >= 20:
-            break
-    med = float(np.median(times))
     cores = int(os.environ.get("OMP_NUM_THREADS", os.environ.get("OPENBLAS_NUM_THREADS", "0")) or 0) \
         or os.cpu_count()
-    return {"value": round(B / med, 1), "unit": "poses/s", "cores": cores, "kind": "port",
-            "sample": f"numpy float32 restatement (oracle/lcn_oracle.py), fwd+bwd+Adam, B={B}, "
-                      f"{len(times)} steps, median {med:.3f} s/step, OpenBLAS threads={cores}"}
+    rng = np.random.default_rng(0)
+    samples = []
+    per_size = seconds / len(batches)
+    est = None  # seconds per pose of the previous size
+    for B in batches:
+        if samples and est is not None and est * B * 3 > seconds:
+            break  # warm-up + two timed steps of this size would not fit the leg
+        x = rng.uniform(-1, 1, (B, 34)).astype(np.float32)
+        lab = rng.uniform(-1, 1, (B, 51)).astype(np.float32)
+        O.train_step(cfg, params, st, x, lab)  # warm-up
+        times = []
+        t_end = time.time() + per_size
+        while (time.time() < t_end or len(times) < 2) and len(times) < 20:
+            t0 = time.perf_counter()
+            O.train_step(cfg, params, st, x, lab)
+            times.append(time.perf_counter() - t0)
+        med = float(np.median(times))
+        est = med / B
+        samples.append({"batch": B, "steps": len(times), "median_s_per_step": round(med, 4),
+                        "poses_per_s": round(B / med, 1)})
+    top = samples[-1]
+    return {"value": top["poses_per_s"], "unit": "poses/s", "cores": cores, "kind": "port",
+            "cpu": _cpu_model(), "blas": _blas_name(), "samples": samples,
+            "sample": f"numpy float32 restatement (oracle/lcn_oracle.py), fwd+bwd+Adam, "
+                      f"B={top['batch']}, {top['steps']} steps, median {top['median_s_per_step']:.3f} "
+                      f"s/step, {_blas_name()} threads={cores}, {_cpu_model()}"}
 
 
 def predict_main(args, rank, world, local):
@@ -160,7 +242,7 @@ def predict_main(args, rank, world, local):
     GPU (flip + rotation: 3 copies, inference.py:70-111) through
     lcn_predict_dataset, batch size = --batch, float64 predictions to the host."""
     from lcn_amd.tta import augment_ops
-    B = args.batch
+    B, G, scaling = batch_plan(args, world, rank)
     neighbour = get_neighbour_matrix_by_hand(neighbour_dict_set[0], knn=args.knn)
     mask = (neighbour.T != 0).astype(np.float32)
     net = native.Network(F=args.channels, in_F=2, num_layers=args.layers, mask_type=args.mask_type,
@@ -184,31 +266,34 @@ def predict_main(args, rank, world, local):
     if rank == 0:
         emit({
             "metric": "poses/sec, TTA predict (flip + rotation, 3 copies per pose)",
-            "value": round(B * world * args.steps / el, 1), "unit": "poses/s", "n_gpus": world,
+            "value": round(G * args.steps / el, 1), "unit": "poses/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic float64 poses resident in HBM; predictions float64 to the host",
             "config": {"workload": f"cfg5-style inference: locally_connected knn={args.knn}, "
                                    f"layers={args.layers}, F={args.channels}, flip+rotation TTA",
-                       "poses_per_gpu": B, "network_batch": B, "copies": 3,
+                       "global_poses": G, "poses_per_gpu": B, "network_batch": B, "copies": 3,
                        "parallelism": f"dp{world} (SyncBN over the ranks' batches)"},
             "finite": bool(np.isfinite(pred).all())})
     net.close()
 
 
-def main():
+def main(argv=None):
     global RESULT_OUT
-    args = parse()
-    RESULT_OUT = _claim_stdout()
-    if args.mode == "predict":
-        rank, world, local = dist_env()
-        return predict_main(args, rank, world, local)
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args, argv)
     rank, world, local = dist_env()
     if world != args.gpus:
-        # launched without torchrun: single process drives one GPU
-        if world == 1 and args.gpus != 1:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE=1; running 1 GPU", file=sys.stderr)
-    B = args.batch
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+              f"(torch.distributed.run --nproc-per-node {args.gpus}) or run plainly", file=sys.stderr)
+        return 2
+    RESULT_OUT = _claim_stdout()
+    if args.mode == "predict":
+        predict_main(args, rank, world, local)
+        return 0
+    B, G, scaling = batch_plan(args, world, rank)
     neighbour = get_neighbour_matrix_by_hand(neighbour_dict_set[0], knn=args.knn)
     if "locally_connected" in args.mask_type:
         mask = (neighbour.T != 0).astype(np.float32)
@@ -285,7 +370,7 @@ def main():
     thost = float(net.allreduce_host([time.perf_counter() - th0], op="max")[0])
 
     ms_step = elapsed / args.steps * 1e3
-    value = B * world * args.steps / elapsed
+    value = G * args.steps / elapsed
     if rank == 0:
         dom = max(kern, key=lambda k: kern[k]["total_ms_per_step"])
         d = kern[dom]
@@ -333,11 +418,11 @@ def main():
         res = {
             "metric": METRIC, "value": round(value, 1), "unit": "poses/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (x~U(-1,1), labels = lifted x + noise), resident in HBM",
-            "config": {"workload": "cfg3: H36M 17-joint LCN train step (fwd+bwd+Adam), "
+            "config": {"workload": f"{args.config}: H36M 17-joint LCN train step (fwd+bwd+Adam), "
                                    f"{args.mask_type} knn={args.knn}",
-                       "global_batch": B * world, "per_gpu_batch": B, "layers": args.layers,
+                       "global_batch": G, "per_gpu_batch": B, "layers": args.layers,
                        "channels": args.channels, "parallelism": f"dp{world} (SyncBN + RCCL grad all-reduce)"
                        + (", one-rank RCCL communicator" if world == 1 and args.rccl_self else "")},
             "roofline": roof,
@@ -345,8 +430,8 @@ def main():
             "hbm_elementwise": hbm_ew,
             "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv for kk, vv in v.items()}
                         for k, v in kern.items()},
-            "fwd_only_poses_per_s": round(B * world * nf / tfwd, 1),
-            "host_input_poses_per_s": round(B * world * nh / thost, 1),
+            "fwd_only_poses_per_s": round(G * nf / tfwd, 1),
+            "host_input_poses_per_s": round(G * nh / thost, 1),
         }
         if args.cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
@@ -354,7 +439,8 @@ def main():
             res["cpu_baseline"] = None
         emit(res)
     net.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define LCN_ABI_VERSION 1
+#define LCN_ABI_VERSION 2
 
 enum {
   LCN_OK = 0,
@@ -159,13 +159,15 @@ int lcn_train_step_indexed(void* handle, int32_t x_slot, int32_t lab_slot, const
  * concatenated as aug->n_copies augmented copies (aug NULL = one plain copy):
  * fixed batches of batch_size, the last zero-padded, batch-statistics BN.
  * With more than one copy the predictions are undone per copy by `undo` and
- * averaged (data.undo).  out: host float64 [N][51].  lab_slot >= 0 (no
+ * averaged (data.undo).  out: host float64 [N][51], N = the dataset's rows;
+ * out_rows is the capacity of `out` in rows (LCN_E_ARG if < N).  lab_slot >= 0 (no
  * augmentation): batch_losses[i] receives batch i's float32 mean loss
  * (losses_cap >= number of batches).  With world > 1 every rank predicts its
  * own shard and the ranks' batch i together form one SyncBN batch. */
 int lcn_predict_dataset(void* handle, int32_t x_slot, int32_t lab_slot, int64_t batch_size,
                         const lcn_augment* aug, const lcn_augment* undo, double* out,
-                        float* batch_losses, int64_t losses_cap, int64_t* n_batches);
+                        int64_t out_rows, float* batch_losses, int64_t losses_cap,
+                        int64_t* n_batches);
 
 /* --- data parallel (RCCL over xGMI) ------------------------------------ */
 /* Replaces the single-process Session of models_att.py:155, 210-212 with one
@@ -178,6 +180,25 @@ int lcn_predict_dataset(void* handle, int32_t x_slot, int32_t lab_slot, int64_t 
  * communicator. */
 int lcn_comm_unique_id(void* id_out /* 128 bytes */);
 int lcn_comm_init(void* handle, const void* id /* 128 bytes */, int32_t rank, int32_t world);
+/* The same data-parallel step over a transport of the caller's: every exchange
+ * (the ranks' row counts, SyncBN sums, the loss, the raw gradient vector)
+ * copies its device buffer to host memory, calls fn -- an in-place all-reduce
+ * of `count` elements (dtype LCN_DTYPE_F32 / LCN_DTYPE_F64; op 0 sum, 1 max)
+ * over the `world` ranks, 0 on success -- and copies the result back, in
+ * stream order.  For ranks that RCCL cannot join (several ranks sharing one
+ * GPU, as the multi-rank tests do; a host-only fabric).  The ranks' batches
+ * may differ in size with either communicator: BN statistics, the loss and
+ * its gradient use the all-reduced global row count.  No counterpart in the
+ * reference (single process, models_att.py:155). */
+typedef int (*lcn_host_allreduce_fn)(void* ctx, void* buf, int64_t count, int32_t dtype, int32_t op);
+int lcn_comm_init_host(void* handle, int32_t rank, int32_t world, lcn_host_allreduce_fn fn, void* ctx);
+/* suspend != 0: until resumed, compute calls on this handle run rank-locally
+ * (no exchange, BN over the call's own batch) -- every rank can then evaluate
+ * the same whole data set with the single-process arithmetic of predict
+ * (models_att.py:79-132) between data-parallel training steps.  Every rank
+ * must suspend / resume at the same point.  lcn_comm_allreduce_host still
+ * exchanges while suspended. */
+int lcn_comm_suspend(void* handle, int32_t suspend);
 int lcn_comm_allreduce_host(void* handle, double* values, int32_t count, int32_t op /* 0 sum, 1 max */);
 
 /* --- evaluation -------------------------------------- */

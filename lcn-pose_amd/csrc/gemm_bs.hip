@@ -304,8 +304,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   // applied to the partials only -- the stored dh stays the incoming gradient
   if constexpr (EPI == kEpiBnBackDrop) {
     const int64_t row = (int64_t)rt * kRT + (lane & 31);
+    const Dropout dr = drop_resolve(a.epi_drop);
 #pragma unroll
-    for (int i = 0; i < 32; ++i) v[i] = drop_apply(a.epi_drop, row, so * kSlab + acc_feature(i, h), v[i]);
+    for (int i = 0; i < 32; ++i) v[i] = drop_apply(dr, row, so * kSlab + acc_feature(i, h), v[i]);
   }
 #define BNBACK_EPI(P)                                                                      \
   {                                                                                        \

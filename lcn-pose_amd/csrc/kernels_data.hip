@@ -195,13 +195,15 @@ void launch_tta_undo(const double* pred, int64_t N, const Augment& undo, double*
 }
 
 // per-batch predict loss (float32, as the reference's fetched batch_loss):
-// losses[i] = (float)(loss_sum / count)
-__global__ void batch_loss_kernel(const double* loss_sum, double count, float* losses, int i) {
-  if (threadIdx.x == 0) losses[i] = (float)(loss_sum[0] / count);
+// losses[i] = (float)(loss_sum / (rows * 51)), rows over all ranks
+__global__ void batch_loss_kernel(const double* loss_sum, double rows, const RowInfo* ri,
+                                  float* losses, int i) {
+  if (threadIdx.x == 0) losses[i] = (float)(loss_sum[0] / ((ri ? ri->rows_global : rows) * 51.0));
 }
 
-void launch_batch_loss(const double* loss_sum, double count, float* losses, int i, hipStream_t s) {
-  hipLaunchKernelGGL(batch_loss_kernel, dim3(1), dim3(64), 0, s, loss_sum, count, losses, i);
+void launch_batch_loss(const double* loss_sum, double rows, const RowInfo* ri, float* losses, int i,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(batch_loss_kernel, dim3(1), dim3(64), 0, s, loss_sum, rows, ri, losses, i);
 }
 
 }  // namespace lcn

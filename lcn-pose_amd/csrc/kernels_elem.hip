@@ -81,12 +81,14 @@ __device__ __forceinline__ void colsum_groups_lds(const double2* __restrict__ co
 // acc[2F] (and stop); 2: finish from the all-reduced acc.  zsum (when given)
 // receives the per-column sums of z (bias-gradient term of the backward).
 __global__ __launch_bounds__(1024) void bn_fwd_finalize_kernel(
-    const double2* __restrict__ col, int H, int F, int phase, double count,
-    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, double* acc,
-    BnStats st, double* __restrict__ zsum) {
+    const double2* __restrict__ col, int H, int F, int phase, double rows,
+    const RowInfo* __restrict__ ri, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, double* acc, BnStats st,
+    double* __restrict__ zsum) {
   extern __shared__ double2 cs[];  // [H]
   if (phase <= 1) colsum_groups_lds(col, H, cs);
   const int J = H / F;
+  const double count = (ri ? ri->rows_global : rows) * (double)J;
   for (int ch = threadIdx.x; ch < F; ch += blockDim.x) {
     double S = 0.0, Q = 0.0;
     if (phase <= 1) {
@@ -113,11 +115,11 @@ __global__ __launch_bounds__(1024) void bn_fwd_finalize_kernel(
   }
 }
 
-void launch_bn_fwd_finalize(const double2* col, int H, int F, int phase, double count,
-                            const float* gamma, const float* beta, float eps, double* acc,
-                            BnStats st, double* zsum, hipStream_t s) {
+void launch_bn_fwd_finalize(const double2* col, int H, int F, int phase, double rows,
+                            const RowInfo* ri, const float* gamma, const float* beta, float eps,
+                            double* acc, BnStats st, double* zsum, hipStream_t s) {
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(1), dim3(1024), H * sizeof(double2), s, col, H,
-                     F, phase, count, gamma, beta, eps, acc, st, zsum);
+                     F, phase, rows, ri, gamma, beta, eps, acc, st, zsum);
 }
 
 // Backward BN finish per channel:  dz = c1*du + c2 + c3*z,
@@ -129,14 +131,15 @@ void launch_bn_fwd_finalize(const double2* col, int H, int F, int phase, double 
 // all-reduced later); c123 uses the global sums.  bn = 0 (no BatchNorm):
 // dz = du and only db is written.  Phases as bn_fwd_finalize.
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
-    const double2* __restrict__ col, int H, int F, int phase, int bn, double count,
-    double b_local, const float* __restrict__ gamma, const float* __restrict__ mean,
-    const float* __restrict__ rstd, double* acc, float* __restrict__ dgamma,
-    float* __restrict__ dbeta, float* __restrict__ c123, const double* __restrict__ zsum,
-    float* __restrict__ db) {
+    const double2* __restrict__ col, int H, int F, int phase, int bn, double rows,
+    const RowInfo* __restrict__ ri, double b_local, const float* __restrict__ gamma,
+    const float* __restrict__ mean, const float* __restrict__ rstd, double* acc,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ c123,
+    const double* __restrict__ zsum, float* __restrict__ db) {
   extern __shared__ double2 cs[];  // [H]
   colsum_groups_lds(col, H, cs);
   const int J = H / F;
+  const double count = (ri ? ri->rows_global : rows) * (double)J;
   for (int ch = threadIdx.x; ch < F; ch += blockDim.x) {
     if (!bn) {
       for (int j = 0; j < J; ++j) db[j * F + ch] = (float)cs[j * F + ch].x;
@@ -170,12 +173,13 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
   }
 }
 
-void launch_bn_bwd_finalize(const double2* col, int H, int F, int phase, int bn, double count,
-                            double b_local, const float* gamma, const float* mean,
-                            const float* rstd, double* acc, float* dgamma, float* dbeta,
-                            float* c123, const double* zsum, float* db, hipStream_t s) {
+void launch_bn_bwd_finalize(const double2* col, int H, int F, int phase, int bn, double rows,
+                            const RowInfo* ri, double b_local, const float* gamma,
+                            const float* mean, const float* rstd, double* acc, float* dgamma,
+                            float* dbeta, float* c123, const double* zsum, float* db,
+                            hipStream_t s) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(1024), H * sizeof(double2), s, col, H,
-                     F, phase, bn, count, b_local, gamma, mean, rstd, acc, dgamma, dbeta, c123,
+                     F, phase, bn, rows, ri, b_local, gamma, mean, rstd, acc, dgamma, dbeta, c123,
                      zsum, db);
 }
 
@@ -187,8 +191,9 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const float4* __restrict__ 
                                                      float4* __restrict__ h,
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int F, int S,
-                                                     float alpha, int64_t n4, Dropout drop) {
+                                                     float alpha, int64_t n4, Dropout drop_in) {
   const int spj = F / 64;
+  const Dropout drop = drop_resolve(drop_in);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     const int c4 = (int)(i & 511);
     const int ch = (int)((i >> 9) % S % spj) * 64 + 8 * (c4 >> 6) + 4 * ((c4 >> 5) & 1);
@@ -255,6 +260,29 @@ __global__ void col_to_float_kernel(const double2* __restrict__ col, int n, floa
 
 void launch_col_to_float(const double2* col, int n, float* out, hipStream_t s) {
   hipLaunchKernelGGL(col_to_float_kernel, dim3((n + 255) / 256), dim3(256), 0, s, col, n, out);
+}
+
+// The ranks' batch rows of a step: begin fills this rank's slot (the others
+// zero), an all-reduce (sum) gathers them, finish derives this rank's RowInfo.
+__global__ void rows_begin_kernel(double* rows, int world, int rank, double B) {
+  const int r = threadIdx.x;
+  if (r < world) rows[r] = r == rank ? B : 0.0;
+}
+__global__ void rows_finish_kernel(const double* rows, int world, int rank, RowInfo* ri) {
+  if (threadIdx.x != 0) return;
+  double total = 0.0, below = 0.0;
+  for (int r = 0; r < world; ++r) {
+    if (r < rank) below += rows[r];
+    total += rows[r];
+  }
+  ri->rows_global = total;
+  ri->row0 = (int64_t)below;
+}
+void launch_rows_begin(double* rows, int world, int rank, int64_t B, hipStream_t s) {
+  hipLaunchKernelGGL(rows_begin_kernel, dim3(1), dim3(256), 0, s, rows, world, rank, (double)B);
+}
+void launch_rows_finish(const double* rows, int world, int rank, RowInfo* ri, hipStream_t s) {
+  hipLaunchKernelGGL(rows_finish_kernel, dim3(1), dim3(64), 0, s, rows, world, rank, ri);
 }
 
 }  // namespace lcn

@@ -65,6 +65,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   f32x16 acc0, acc1;
 #pragma unroll
   for (int k = 0; k < 16; ++k) { acc0[k] = 0.f; acc1[k] = 0.f; }
+  [[maybe_unused]] Dropout dr{};
+  if constexpr (DROP) dr = drop_resolve(a.d_drop);
 
   // this thread's staging slots: j = 0, 1 -> chunk g = w + 4j of the stage's
   // row tile, lane `lane`: row lr, features f0 + 32j .. +3
@@ -115,14 +117,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
       if constexpr (DROP) {  // tf.nn.dropout's gradient: dh * mask * scale
         const int64_t row = base + lr;
         const int col = so * kSlab + f0;
-        rd0.x = drop_apply(a.d_drop, row, col, rd0.x);
-        rd0.y = drop_apply(a.d_drop, row, col + 1, rd0.y);
-        rd0.z = drop_apply(a.d_drop, row, col + 2, rd0.z);
-        rd0.w = drop_apply(a.d_drop, row, col + 3, rd0.w);
-        rd1.x = drop_apply(a.d_drop, row, col + 32, rd1.x);
-        rd1.y = drop_apply(a.d_drop, row, col + 33, rd1.y);
-        rd1.z = drop_apply(a.d_drop, row, col + 34, rd1.z);
-        rd1.w = drop_apply(a.d_drop, row, col + 35, rd1.w);
+        rd0.x = drop_apply(dr, row, col, rd0.x);
+        rd0.y = drop_apply(dr, row, col + 1, rd0.y);
+        rd0.z = drop_apply(dr, row, col + 2, rd0.z);
+        rd0.w = drop_apply(dr, row, col + 3, rd0.w);
+        rd1.x = drop_apply(dr, row, col + 32, rd1.x);
+        rd1.y = drop_apply(dr, row, col + 33, rd1.y);
+        rd1.z = drop_apply(dr, row, col + 34, rd1.z);
+        rd1.w = drop_apply(dr, row, col + 35, rd1.w);
       }
       rd0 = bnback4(rd0, rz0, coef(f0), a.alpha);
       rd1 = bnback4(rd1, rz1, coef(f0 + 32), a.alpha);

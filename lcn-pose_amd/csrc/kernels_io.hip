@@ -17,6 +17,8 @@ __global__ __launch_bounds__(256) void out_assemble_kernel(OutAsmArgs a) {
   __shared__ double red[4];
   const int t = threadIdx.x, c = t & 63, w = t >> 6;
   const int j = c / 3, k = c - 3 * j;
+  // d out = 2 (out - lab) / (rows * 51), rows over all ranks
+  const float dscale = (float)(2.0 / ((a.ri ? a.ri->rows_global : a.rows) * 51.0));
   double lsum = 0.0;
   for (int row = blockIdx.x * 4 + w; row < a.B; row += gridDim.x * 4) {
     if (c < 51) {
@@ -26,7 +28,7 @@ __global__ __launch_bounds__(256) void out_assemble_kernel(OutAsmArgs a) {
       if (a.lab) {
         const float d = o - a.lab[(size_t)row * 51 + c];
         lsum += (double)d * (double)d;
-        if (a.dy) a.dy[tix(row, c, 1)] = a.dscale * d;
+        if (a.dy) a.dy[tix(row, c, 1)] = dscale * d;
       }
     } else if (a.dy) {
       a.dy[tix(row, c, 1)] = 0.f;  // padded columns of the output layer's dX operand

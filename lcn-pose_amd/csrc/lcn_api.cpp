@@ -135,9 +135,16 @@ struct Handle {
   float* batch_losses = nullptr;  // [loss_cap] per-batch predict losses
   int64_t pred_rows = 0, loss_cap = 0;
 
-  // communication
+  // communication: an RCCL communicator (lcn_comm_init) or a host exchange
+  // (lcn_comm_init_host: every all-reduce goes through the caller's function)
   ncclComm_t comm = nullptr;
+  lcn_host_allreduce_fn host_ar = nullptr;
+  void* host_ctx = nullptr;
+  std::vector<char> host_stage;
   int rank = 0, world = 1;
+  bool comm_off = false;          // lcn_comm_suspend: calls run rank-locally
+  double* rows_all = nullptr;     // [world] the ranks' batch rows of the running step
+  RowInfo* rowinfo = nullptr;     // global rows / first global row of this rank (device)
   // run the multi-GPU (phase 1 -> all-reduce -> phase 2) BN reductions without
   // a communicator (LCN_FORCE_PHASED=1 at create); with one (lcn_comm_init,
   // any world size) they always run phased
@@ -482,6 +489,7 @@ int build(Handle* h, const lcn_config* c) {
   CHECK(dalloc(h, &h->loss_sum, 4));
   CHECK(dalloc(h, &h->acc1, 2 * F));
   CHECK(dalloc(h, &h->acc2, 2 * F));
+  CHECK(dalloc(h, &h->rowinfo, 1));
   const size_t dw_elems = std::max((size_t)dw_chunks(h->nblk) * h->nblk,
                                    (size_t)dw_chunks(h->nslab) * h->nslab) * 4096;
   CHECK(dalloc(h, &h->dw_part, dw_elems));
@@ -491,11 +499,49 @@ int build(Handle* h, const lcn_config* c) {
 // ---------------------------------------------------------------------------
 // step pieces
 // ---------------------------------------------------------------------------
+// several ranks (or a one-rank communicator): the step runs the phased BN
+// reductions and every exchange below
+bool has_comm(const Handle* h) { return h->comm != nullptr || h->host_ar != nullptr; }
+bool multi(const Handle* h) { return has_comm(h) && !h->comm_off; }
+
+// In-place all-reduce of a device buffer over the ranks, stream-ordered: RCCL,
+// or (host exchange) device -> host, the caller's function, host -> device.
 int allreduce(Handle* h, void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op = ncclSum) {
-  if (!h->comm) return LCN_OK;
-  NCCLC(ncclAllReduce(buf, buf, count, dt, op, h->comm, h->stream));
+  if (h->comm) {
+    NCCLC(ncclAllReduce(buf, buf, count, dt, op, h->comm, h->stream));
+    return LCN_OK;
+  }
+  if (!h->host_ar) return LCN_OK;
+  const size_t bytes = count * (dt == ncclDouble ? 8 : 4);
+  if (h->host_stage.size() < bytes) h->host_stage.resize(bytes);
+  HIPC(hipMemcpyAsync(h->host_stage.data(), buf, bytes, hipMemcpyDeviceToHost, h->stream));
+  HIPC(hipStreamSynchronize(h->stream));
+  const int rc = h->host_ar(h->host_ctx, h->host_stage.data(), (int64_t)count,
+                            dt == ncclDouble ? LCN_DTYPE_F64 : LCN_DTYPE_F32, op == ncclMax ? 1 : 0);
+  if (rc != 0) {
+    h->err = "host all-reduce callback failed (" + std::to_string(rc) + ")";
+    return LCN_E_COMM;
+  }
+  HIPC(hipMemcpyAsync(buf, h->host_stage.data(), bytes, hipMemcpyHostToDevice, h->stream));
+  // the staging buffer is reused by the next exchange
+  HIPC(hipStreamSynchronize(h->stream));
   return LCN_OK;
 }
+
+// The ranks' shards may differ in size: gather every rank's batch rows (an
+// all-reduce of a one-hot vector) and derive the global row count and this
+// rank's first global row on the device (RowInfo), where the BN finishes, the
+// loss scale and the dropout keys read them.
+int exchange_rows(Handle* h, int64_t B) {
+  if (!multi(h)) return LCN_OK;
+  launch_rows_begin(h->rows_all, h->world, h->rank, B, h->stream);
+  CHECK(allreduce(h, h->rows_all, (size_t)h->world, ncclDouble));
+  launch_rows_finish(h->rows_all, h->world, h->rank, h->rowinfo, h->stream);
+  return LCN_OK;
+}
+// what the kernels take: the device RowInfo with several ranks, else null
+// (then the by-value local row count is the global one)
+const RowInfo* rinfo(const Handle* h) { return multi(h) ? h->rowinfo : nullptr; }
 
 void tstart(Handle* h, int k, hipEvent_t* pair) {
   if (!h->timing) return;
@@ -523,7 +569,9 @@ Dropout drop_of(const Handle* h, int k, int64_t B) {
   d.scale = h->drop_scale;
   d.lseed = fmix32(h->step_seed ^ ((uint32_t)(k + 1) * 0x9e3779b9u));
   d.H = h->H;
-  d.row0 = (int64_t)h->rank * B;
+  d.row0 = 0;
+  d.ri = rinfo(h);
+  (void)B;
   return d;
 }
 
@@ -542,19 +590,20 @@ int prep_weights(Handle* h) {
 int bn_stats(Handle* h, int k, int B) {
   if (!h->batch_norm) return LCN_OK;
   hipStream_t s = h->stream;
-  const double count = (double)B * h->world * kJ;
+  const double rows = (double)B;
+  const RowInfo* ri = rinfo(h);
   const float* gamma = h->theta + h->gamma_off[k];
   const float* beta = h->theta + h->beta_off[k];
   launch_colreduce(h->stat_part, (int)cdiv(B, kGemmRows), kGemmRows, B, h->H, 1, h->colacc, s);
-  if (!h->phased && !h->comm) {
-    launch_bn_fwd_finalize(h->colacc, h->H, h->F, 0, count, gamma, beta, h->eps, h->acc1, h->bn[k],
+  if (!h->phased && !multi(h)) {
+    launch_bn_fwd_finalize(h->colacc, h->H, h->F, 0, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
                            h->zsum[k], s);
     return LCN_OK;
   }
-  launch_bn_fwd_finalize(h->colacc, h->H, h->F, 1, count, gamma, beta, h->eps, h->acc1, h->bn[k],
+  launch_bn_fwd_finalize(h->colacc, h->H, h->F, 1, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
                          h->zsum[k], s);
   CHECK(allreduce(h, h->acc1, 2 * h->F, ncclDouble));
-  launch_bn_fwd_finalize(h->colacc, h->H, h->F, 2, count, gamma, beta, h->eps, h->acc1, h->bn[k],
+  launch_bn_fwd_finalize(h->colacc, h->H, h->F, 2, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
                          nullptr, s);
   return LCN_OK;
 }
@@ -694,21 +743,22 @@ int bn_back(Handle* h, int k, int B) {
   hipStream_t s = h->stream;
   const BnStats& st = h->bn[k];
   const int bn = h->batch_norm;
-  const double count = (double)B * h->world * kJ;
+  const double rows = (double)B;
+  const RowInfo* ri = rinfo(h);
   const float* gamma = bn ? h->theta + h->gamma_off[k] : nullptr;
   float* dgam = bn ? h->rg + h->gamma_off[k] : nullptr;
   float* dbet = bn ? h->rg + h->beta_off[k] : nullptr;
   float* db = h->rg + h->b_off[k];
   launch_colreduce(h->stat_part, (int)cdiv(B, kGemmRows), kGemmRows, B, h->H, 0, h->colacc, s);
-  if ((!h->phased && !h->comm) || !bn) {
-    launch_bn_bwd_finalize(h->colacc, h->H, h->F, 0, bn, count, (double)B, gamma, st.mean, st.rstd,
+  if ((!h->phased && !multi(h)) || !bn) {
+    launch_bn_bwd_finalize(h->colacc, h->H, h->F, 0, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
                            h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
     return LCN_OK;
   }
-  launch_bn_bwd_finalize(h->colacc, h->H, h->F, 1, bn, count, (double)B, gamma, st.mean, st.rstd,
+  launch_bn_bwd_finalize(h->colacc, h->H, h->F, 1, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
                          h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
   CHECK(allreduce(h, h->acc1, 2 * h->F, ncclDouble));
-  launch_bn_bwd_finalize(h->colacc, h->H, h->F, 2, bn, count, (double)B, gamma, st.mean, st.rstd,
+  launch_bn_bwd_finalize(h->colacc, h->H, h->F, 2, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
                          h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
   return LCN_OK;
 }
@@ -728,6 +778,7 @@ int forward(Handle* h, int B, bool with_labels, bool train) {
   const int S = h->nslab, nl = h->nl;
   // tf.nn.dropout runs in training steps only (predict feeds rate 0, :102)
   h->drop_on = train && h->drop_rate > 0.f;
+  CHECK(exchange_rows(h, B));
   CHECK(prep_weights(h));
   const int epi = h->batch_norm ? EPI_BNFWD : EPI_NONE;
   // lift z0 = x . W1e + b1 (models_att.py:714-729): x padded to one 64-wide slab
@@ -766,7 +817,8 @@ int forward(Handle* h, int B, bool with_labels, bool train) {
   oa.out = h->out;
   oa.dy = train ? h->dy : nullptr;
   oa.loss_part = with_labels ? h->loss_part : nullptr;
-  oa.dscale = (float)(2.0 / ((double)B * h->world * 51.0));
+  oa.rows = (double)B;
+  oa.ri = rinfo(h);
   oa.B = B;
   const int ogrid = (int)std::min<int64_t>(h->loss_grid, cdiv(B, 4));
   launch_out_assemble(oa, ogrid, s);
@@ -821,9 +873,7 @@ int backward(Handle* h, int B) {
 // the device side of the update: mask / clip backward, Adam (lr_t from lr_dev)
 int finish_device(Handle* h, bool update, bool keep_grads) {
   hipStream_t s = h->stream;
-  if (h->comm) {
-    CHECK(allreduce(h, h->rg, (size_t)h->P, ncclFloat));
-  }
+  if (multi(h)) CHECK(allreduce(h, h->rg, (size_t)h->P, ncclFloat));
   launch_wdot(h->rg, h->theta, h->w_offs, h->w_kin, h->w_nout, h->nl, h->blocksum, s);
   launch_maskgrad(h->blocksum, h->nl, h->Md, h->Sd, h->Cd, h->learnable, h->denom, h->norm2,
                   h->max_norm, h->learnable ? h->rg + h->mask_off : nullptr, h->lcoef, s);
@@ -1026,13 +1076,16 @@ int lcn_forward(void* handle, const float* x, float* out, int64_t B, int32_t fla
 static int read_loss(Handle* h, int64_t B, float* loss) {
   if (!loss) return LCN_OK;
   double v = 0.0;
+  RowInfo ri{(double)B, 0};
   std::vector<double> n2(2 * h->nl, 0.0);
   HIPC(hipMemcpyAsync(&v, h->loss_sum, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  if (multi(h))  // the mean is over every rank's rows
+    HIPC(hipMemcpyAsync(&ri, h->rowinfo, sizeof(ri), hipMemcpyDeviceToHost, h->stream));
   if (h->reg != 0.f)
     HIPC(hipMemcpyAsync(n2.data(), h->norm2, n2.size() * sizeof(double), hipMemcpyDeviceToHost,
                         h->stream));
   HIPC(hipStreamSynchronize(h->stream));
-  double l = v / ((double)B * h->world * 51.0);
+  double l = v / (ri.rows_global * 51.0);
   if (h->reg != 0.f) {
     double r = 0.0;
     for (double x : n2) r += x / 2.0;
@@ -1049,7 +1102,7 @@ int lcn_forward_loss(void* handle, const float* x, const float* labels, float* o
   HIPC(hipSetDevice(h->device));
   CHECK(stage_inputs(h, x, labels, B, flags));
   CHECK(forward(h, (int)B, true, false));
-  if (h->comm) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
+  if (multi(h)) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
   CHECK(finish_launches(h));
   CHECK(copy_out(h, out, B, flags));
   CHECK(read_loss(h, B, loss));
@@ -1060,7 +1113,7 @@ int lcn_forward_loss(void* handle, const float* x, const float* labels, float* o
 // forward, loss, backward and update of one step, enqueued on the stream
 static int enqueue_step(Handle* h, int64_t B, bool update, bool keep) {
   CHECK(forward(h, (int)B, true, true));
-  if (h->comm) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
+  if (multi(h)) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
   CHECK(backward(h, (int)B));
   return finish_device(h, update, keep);
 }
@@ -1095,7 +1148,7 @@ static int run_train_step(Handle* h, int64_t B, int32_t flags, float* loss_out, 
   std::memcpy(&lr_bits, &lr_t, 4);
   HIPC(hipMemsetD32Async((hipDeviceptr_t)h->lr_dev, (int)lr_bits, 1, h->stream));
   hipGraphExec_t exec = nullptr;
-  if (h->use_graphs && !h->comm && !h->timing && h->drop_rate == 0.f &&
+  if (h->use_graphs && !multi(h) && !h->timing && h->drop_rate == 0.f &&
       step_graph(h, B, update, keep, &exec) != LCN_OK) {
     // capture unavailable: fall back to direct launches for this handle
     std::fprintf(stderr, "liblcn: step graph disabled (%s)\n", h->err.c_str());
@@ -1235,7 +1288,8 @@ int lcn_train_step_indexed(void* handle, int32_t x_slot, int32_t lab_slot, const
 
 int lcn_predict_dataset(void* handle, int32_t x_slot, int32_t lab_slot, int64_t batch_size,
                         const lcn_augment* aug, const lcn_augment* undo, double* out,
-                        float* batch_losses, int64_t losses_cap, int64_t* n_batches) {
+                        int64_t out_rows, float* batch_losses, int64_t losses_cap,
+                        int64_t* n_batches) {
   Handle* h = (Handle*)handle;
   if (!h || !out) return LCN_E_ARG;
   HIPC(hipSetDevice(h->device));
@@ -1253,8 +1307,12 @@ int lcn_predict_dataset(void* handle, int32_t x_slot, int32_t lab_slot, int64_t 
     return LCN_E_ARG;
   }
   const int64_t N = dx->rows, total = N * a.n_copies;
+  if (out_rows < N) {
+    h->err = "out holds " + std::to_string(out_rows) + " rows, the dataset has " + std::to_string(N);
+    return LCN_E_ARG;
+  }
   int64_t nb = cdiv(total, batch_size);
-  if (h->comm) {  // every rank runs the same number of (SyncBN) batches
+  if (multi(h)) {  // every rank runs the same number of (SyncBN) batches
     double v = (double)nb;
     CHECK(lcn_comm_allreduce_host(h, &v, 1, 1));
     nb = (int64_t)v;
@@ -1292,9 +1350,8 @@ int lcn_predict_dataset(void* handle, int32_t x_slot, int32_t lab_slot, int64_t 
     CHECK(gather_batch(h, dx, dl, nullptr, begin, a, batch_size));
     CHECK(forward(h, (int)batch_size, dl != nullptr, false));
     if (dl) {
-      if (h->comm) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
-      launch_batch_loss(h->loss_sum, (double)batch_size * h->world * 51.0, h->batch_losses, (int)i,
-                        h->stream);
+      if (multi(h)) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
+      launch_batch_loss(h->loss_sum, (double)batch_size, rinfo(h), h->batch_losses, (int)i, h->stream);
     }
     const int64_t n = std::min<int64_t>(batch_size, total - begin);
     if (n > 0) launch_store_pred(h->out, n, h->pred + begin * 51, h->stream);
@@ -1375,8 +1432,9 @@ int lcn_comm_unique_id(void* id_out) {
 int lcn_comm_init(void* handle, const void* id_in, int32_t rank, int32_t world) {
   Handle* h = (Handle*)handle;
   if (!h || !id_in || world < 1 || rank < 0 || rank >= world) return LCN_E_ARG;
-  if (h->comm) { h->err = "lcn_comm_init: the handle already has a communicator"; return LCN_E_ARG; }
+  if (has_comm(h)) { h->err = "lcn_comm_init: the handle already has a communicator"; return LCN_E_ARG; }
   HIPC(hipSetDevice(h->device));
+  CHECK(dalloc(h, &h->rows_all, (size_t)world));
   // a real communicator even at world 1: every exchange below is gated on
   // h->comm, so a one-GPU run after comm_init takes the multi-GPU code path
   // (phased BN reductions, RCCL all-reduces) end to end
@@ -1388,12 +1446,41 @@ int lcn_comm_init(void* handle, const void* id_in, int32_t rank, int32_t world) 
   return LCN_OK;
 }
 
+int lcn_comm_init_host(void* handle, int32_t rank, int32_t world, lcn_host_allreduce_fn fn, void* ctx) {
+  Handle* h = (Handle*)handle;
+  if (!h || !fn || world < 1 || rank < 0 || rank >= world) return LCN_E_ARG;
+  if (has_comm(h)) { h->err = "lcn_comm_init_host: the handle already has a communicator"; return LCN_E_ARG; }
+  HIPC(hipSetDevice(h->device));
+  CHECK(dalloc(h, &h->rows_all, (size_t)world));
+  h->host_ar = fn;
+  h->host_ctx = ctx;
+  h->rank = rank;
+  h->world = world;
+  return LCN_OK;
+}
+
+int lcn_comm_suspend(void* handle, int32_t suspend) {
+  Handle* h = (Handle*)handle;
+  if (!h) return LCN_E_ARG;
+  HIPC(hipSetDevice(h->device));
+  HIPC(hipStreamSynchronize(h->stream));
+  h->comm_off = suspend != 0;
+  return LCN_OK;
+}
+
 int lcn_comm_allreduce_host(void* handle, double* values, int32_t count, int32_t op) {
   Handle* h = (Handle*)handle;
   if (!h || !values || count <= 0 || count > 2 * h->F) return LCN_E_ARG;
-  if (!h->comm) return LCN_OK;
+  if (!has_comm(h)) return LCN_OK;
   HIPC(hipSetDevice(h->device));
   HIPC(hipStreamSynchronize(h->stream));
+  if (h->host_ar) {  // host values: no device round trip
+    if (h->host_ar(h->host_ctx, values, count, LCN_DTYPE_F64, op == 1 ? 1 : 0) != 0) {
+      h->err = "host all-reduce callback failed";
+      return LCN_E_COMM;
+    }
+    return LCN_OK;
+  }
   HIPC(hipMemcpy(h->acc2, values, count * sizeof(double), hipMemcpyHostToDevice));
   NCCLC(ncclAllReduce(h->acc2, h->acc2, count, ncclDouble, op == 1 ? ncclMax : ncclSum, h->comm,
                       h->stream));

@@ -53,13 +53,28 @@ __host__ __device__ inline int frag_ix(int n, int k) {
 // scale = float(1 / (1 - rate)), as TF's dropout computes it, a dropped one 0.
 // oracle/lcn_oracle.py restates the same function (dropout_mask).
 // ----------------------------------------------------------------------------
+// Rows of the running step over all data-parallel ranks.  With several ranks
+// the shards may differ in size, so the global row count (BN statistics, loss
+// scale) and this rank's first global row (dropout keys) are exchanged on the
+// device at the start of every step and read from here by the kernels.
+struct RowInfo {
+  double rows_global;   // sum of the ranks' batch rows
+  int64_t row0;         // rows of the ranks below this one
+};
+
 struct Dropout {
   uint32_t lseed;   // per step and BN layer
   float rate;       // 0 = off
   float scale;
   int H;            // columns of the layer (17 * F)
-  int64_t row0;     // global row of local row 0 (rank offset)
+  int64_t row0;     // global row of local row 0 (rank offset) when ri is null
+  const RowInfo* ri;  // several ranks: row0 is read from device memory
 };
+// the kernel-side copy with row0 resolved (one scalar load per kernel)
+__device__ inline Dropout drop_resolve(Dropout d) {
+  if (d.ri) d.row0 = d.ri->row0;
+  return d;
+}
 __host__ __device__ inline uint32_t fmix32(uint32_t x) {
   x ^= x >> 16; x *= 0x85ebca6bu; x ^= x >> 13; x *= 0xc2b2ae35u; x ^= x >> 16;
   return x;
@@ -153,7 +168,8 @@ struct OutAsmArgs {
   float* out;                        // [B][51] row-major
   float* dy;                         // 1-slab tiled, or null (padding written as 0)
   double* loss_part;                 // [gridDim] or null
-  float dscale;                      // 2 / (B_global * 51)
+  double rows;                       // global batch rows: dy = 2 (out - lab) / (rows * 51)
+  const RowInfo* ri;                 // several ranks: rows read from device memory
   int B;
 };
 void launch_out_assemble(const OutAsmArgs& a, int grid, hipStream_t s);
@@ -181,7 +197,14 @@ void launch_gather_rows(const void* ds, int dtype, int64_t rows, int cols, const
                         int64_t base, int B, float* dst, hipStream_t s);
 void launch_store_pred(const float* out, int64_t n, double* pred, hipStream_t s);
 void launch_tta_undo(const double* pred, int64_t N, const Augment& undo, double* out, hipStream_t s);
-void launch_batch_loss(const double* loss_sum, double count, float* losses, int i, hipStream_t s);
+// losses[i] = (float)(loss_sum / (rows * 51)); rows from ri when given
+void launch_batch_loss(const double* loss_sum, double rows, const RowInfo* ri, float* losses, int i,
+                       hipStream_t s);
+// rows[r] = (r == rank ? B : 0) for r < world: the all-reduce (sum) of it is the
+// all-gather of the ranks' batch rows
+void launch_rows_begin(double* rows, int world, int rank, int64_t B, hipStream_t s);
+// rows[world] of every rank -> RowInfo of this rank
+void launch_rows_finish(const double* rows, int world, int rank, RowInfo* ri, hipStream_t s);
 // evaluate.py per-frame, per-joint error (kernels_eval.hip): pred / gt [n][17][3],
 // box [n][4], cam [n][4] = (cx, cy, fx, fy), root_depth [n] -> err [n][17]
 void launch_mpjpe(int64_t n, const double* pred, const double* gt, const double* box, const double* cam,
@@ -199,15 +222,17 @@ constexpr int kColSplit = 8;
 void launch_colreduce(const float2* part, int n_tiles, int tile_rows, int B, int H, int mode,
                       double2* out, hipStream_t s);
 // forward BN finish from colreduce mode-1 sums.  phase 0 complete (single GPU);
-// 1 local channel sums -> acc[2F]; 2 finish from all-reduced acc.  count =
-// rows_global * J.  zsum (optional): per-column sum of z.
-void launch_bn_fwd_finalize(const double2* col, int H, int F, int phase, double count,
+// 1 local channel sums -> acc[2F]; 2 finish from all-reduced acc.  The element
+// count per channel is rows_global * J, rows_global = `rows` or, when ri is
+// given, ri->rows_global.  zsum (optional): per-column sum of z.
+void launch_bn_fwd_finalize(const double2* col, int H, int F, int phase, double rows,
+                            const RowInfo* ri,
                             const float* gamma, const float* beta, float eps, double* acc,
                             BnStats st, double* zsum, hipStream_t s);
 // backward BN finish from colreduce mode-0 sums of (du, du*zhat): c1|c2|c3,
 // local dgamma/dbeta and the bias gradient db; bn = 0: db = sum du only
-void launch_bn_bwd_finalize(const double2* col, int H, int F, int phase, int bn, double count,
-                            double b_local, const float* gamma, const float* mean,
+void launch_bn_bwd_finalize(const double2* col, int H, int F, int phase, int bn, double rows,
+                            const RowInfo* ri, double b_local, const float* gamma, const float* mean,
                             const float* rstd, double* acc, float* dgamma, float* dbeta,
                             float* c123, const double* zsum, float* db, hipStream_t s);
 // h = [res +] leaky(scale*z + shift), tiled [B][S*64] buffers

@@ -87,8 +87,9 @@ def main():
 
     result = datareader.denormalize(predictions)
     save_path = os.path.join(ROOT_PATH, 'experiment', params['dir_name'], 'result.pkl')
-    with open(save_path, 'wb') as f:
-        pickle.dump(result, f)
+    if int(os.environ.get("RANK", "0")) == 0:  # one process per GPU: every rank predicted the same
+        with open(save_path, 'wb') as f:
+            pickle.dump(result, f)
 
 
 if __name__ == '__main__':

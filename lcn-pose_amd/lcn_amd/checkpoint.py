@@ -14,8 +14,11 @@ variable names the reference graph gives its variables (``tf_name_map``):
   linear_model/two_linear_<i>/batch_normalization{1,2}<i>/...    (:664-697)
   <var>/Adam, <var>/Adam_1                     AdamOptimizer slots m, v
   beta1_power, beta2_power, global_step        Adam / training state (:386-409)
-  loss/{mse_loss/Mean,add}/ExponentialMovingAverage[/biased,/local_step]
-                                               loss EMA(0.9) (:368-379)
+  loss/{mse_loss/Mean,add}/ExponentialMovingAverage
+                                               loss EMA(0.9) shadows (:368-379):
+                                               zero-initialised, zero_debias off
+                                               (the v1 default), so no /biased or
+                                               /local_step companions exist
 
 Keras BN moving statistics are written as their initial values (0, 1): the
 reference never runs their update ops (it trains and predicts with batch
@@ -86,13 +89,10 @@ def to_tensors(net, loss_ema=None, regularized=False) -> Dict[str, np.ndarray]:
     t["beta1_power"] = np.float32(b1p).reshape(())
     t["beta2_power"] = np.float32(b2p).reshape(())
     t["global_step"] = np.int32(gs).reshape(())
-    biased, steps = loss_ema if loss_ema else (0.0, 0)
-    avg = biased / (1 - 0.9 ** steps) if steps else 0.0
+    # the shadow of a tensor starts at 0 and is never debiased (zero_debias=False)
+    shadow = loss_ema[0] if loss_ema else 0.0
     for op in _ema_names(regularized):
-        base = op + "/ExponentialMovingAverage"
-        t[base] = np.float32(avg).reshape(())
-        t[base + "/biased"] = np.float32(biased).reshape(())
-        t[base + "/local_step"] = np.float32(steps).reshape(())
+        t[op + "/ExponentialMovingAverage"] = np.float32(shadow).reshape(())
     return t
 
 
@@ -141,7 +141,7 @@ def _exists(prefix: str) -> bool:
 
 def restore(net, prefix: str) -> Optional[Tuple[float, int]]:
     """Saver.restore: parameters, Adam slots, beta powers, global_step.
-    Returns the loss EMA state (biased, steps) when the checkpoint has one."""
+    Returns the loss EMA state (shadow, 0) when the checkpoint has one."""
     if prefix.endswith(".npz") or (not os.path.exists(prefix + ".index")
                                    and os.path.exists(prefix + ".npz")):
         return _restore_npz(net, prefix)
@@ -163,8 +163,8 @@ def restore(net, prefix: str) -> Optional[Tuple[float, int]]:
                             float(t.get("beta1_power", 0.9)), float(t.get("beta2_power", 0.999)))
     for op in ("loss/add", "loss/add_1"):  # the total loss's EMA
         base = op + "/ExponentialMovingAverage"
-        if base + "/biased" in t:
-            return float(t[base + "/biased"]), int(t[base + "/local_step"])
+        if base in t:
+            return float(t[base]), 0
     return None
 
 

@@ -15,7 +15,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LCN_LIB", os.path.join(HERE, "liblcn.so"))
 
-LCN_ABI_VERSION = 1
+LCN_ABI_VERSION = 2
 MASK_LOCALLY_CONNECTED, MASK_EXPONENTIAL = 0, 1
 IN_DEVICE, OUT_DEVICE, NO_UPDATE, KEEP_GRADS, ASYNC = 1, 2, 4, 8, 16
 K_GEMM_FWD, K_GEMM_DX, K_GEMM_DW, K_BN_ACT = 0, 1, 2, 3
@@ -55,6 +55,9 @@ def make_augment(ops) -> LcnAugment:
     return a
 
 
+# lcn_host_allreduce_fn: int (*)(void* ctx, void* buf, int64 count, int32 dtype, int32 op)
+HOST_ALLREDUCE_FN = ctypes.CFUNCTYPE(_i32, _vp, _vp, _i64, _i32, _i32)
+
 SIGNATURES = {
     "lcn_abi_version": ([], _i32),
     "lcn_create": ([ctypes.POINTER(LcnConfig), _i32, ctypes.POINTER(_vp)], _i32),
@@ -78,9 +81,11 @@ SIGNATURES = {
     "lcn_dataset_free": ([_vp, _i32], _i32),
     "lcn_train_step_indexed": ([_vp, _i32, _i32, _vp, _i64, _i32, _f32p, _f32p], _i32),
     "lcn_predict_dataset": ([_vp, _i32, _i32, _i64, ctypes.POINTER(LcnAugment),
-                             ctypes.POINTER(LcnAugment), _f64p, _f32p, _i64, _i64p], _i32),
+                             ctypes.POINTER(LcnAugment), _f64p, _i64, _f32p, _i64, _i64p], _i32),
     "lcn_comm_unique_id": ([_vp], _i32),
     "lcn_comm_init": ([_vp, _vp, _i32, _i32], _i32),
+    "lcn_comm_init_host": ([_vp, _i32, _i32, HOST_ALLREDUCE_FN, _vp], _i32),
+    "lcn_comm_suspend": ([_vp, _i32], _i32),
     "lcn_comm_allreduce_host": ([_vp, _f64p, _i32, _i32], _i32),
     "lcn_crc32c": ([ctypes.c_uint32, ctypes.c_char_p, _i64], ctypes.c_uint32),
     "lcn_set_dropout": ([_vp, ctypes.c_float, ctypes.c_uint64], _i32),
@@ -348,7 +353,7 @@ class Network:
         u = make_augment(undo) if undo else None
         self._check(self.lib.lcn_predict_dataset(
             self.h, x_slot, lab_slot, batch_size, ctypes.byref(a) if a else None,
-            ctypes.byref(u) if u else None, out.ctypes.data_as(_f64p),
+            ctypes.byref(u) if u else None, out.ctypes.data_as(_f64p), n_rows,
             _fp(losses) if lab_slot >= 0 else None, nb_cap, ctypes.byref(nb)))
         if lab_slot >= 0:
             return out, losses[:nb.value]
@@ -367,6 +372,29 @@ class Network:
     def comm_init(self, uid: bytes, rank: int, world: int):
         buf = ctypes.create_string_buffer(uid, 128)
         self._check(self.lib.lcn_comm_init(self.h, buf, rank, world))
+
+    def comm_init_host(self, rank: int, world: int, allreduce):
+        """Data parallel over a transport of the caller's (lcn_comm_init_host):
+        allreduce(array, op) reduces the 1-D float32 / float64 numpy array in
+        place over the ranks (op "sum" or "max") -- e.g. a gloo all_reduce of a
+        CPU tensor sharing the array's memory.  An exception inside it fails
+        the running liblcn call with LCN_E_COMM."""
+        def cb(_ctx, buf, count, dtype, op):
+            try:
+                ct = ctypes.c_double if dtype == DTYPE_F64 else ctypes.c_float
+                arr = np.ctypeslib.as_array(ctypes.cast(buf, ctypes.POINTER(ct)), shape=(int(count),))
+                allreduce(arr, "max" if op == 1 else "sum")
+                return 0
+            except Exception:  # noqa: BLE001 -- must not propagate through the C frame
+                import traceback
+                traceback.print_exc()
+                return -1
+        self._host_cb = HOST_ALLREDUCE_FN(cb)  # keep the thunk alive as long as the handle
+        self._check(self.lib.lcn_comm_init_host(self.h, rank, world, self._host_cb, None))
+
+    def comm_suspend(self, suspend: bool = True):
+        """Run the following compute calls rank-locally (lcn_comm_suspend)."""
+        self._check(self.lib.lcn_comm_suspend(self.h, int(bool(suspend))))
 
     def allreduce_host(self, values, op="sum") -> np.ndarray:
         v = np.ascontiguousarray(values, dtype=np.float64).copy()

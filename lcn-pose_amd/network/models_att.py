@@ -13,7 +13,13 @@ Deliberate differences from the reference, all documented in DESIGN.md:
     reference re-runs the initializer after restoring, :177-180);
   * checkpoints are TensorFlow tensor bundles written without TensorFlow
     (lcn_amd.checkpoint / tf_bundle: the .index / .data files and variable
-    names of tf.train.Saver, no .meta graph).
+    names of tf.train.Saver, no .meta graph);
+  * launched as one process per GPU (WORLD_SIZE > 1, e.g. torch.distributed.run
+    train.py ...), fit trains data parallel: every rank draws the same batch
+    permutation and steps its contiguous shard of each batch_size batch with
+    SyncBN and an RCCL gradient all-reduce, which keeps the single-process
+    arithmetic (the reference has no parallelism, :155, :210-212); predict /
+    evaluate run the whole set on every rank; only rank 0 prints and writes.
 """
 from __future__ import annotations
 
@@ -26,6 +32,7 @@ import time
 import numpy as np
 
 from lcn_amd import checkpoint as ckpt
+from lcn_amd import dist
 from lcn_amd.init import init_flat
 from lcn_amd.native import Network
 
@@ -57,6 +64,14 @@ def get_exponential_matrix(verbose=True):
     return exp_mat.astype(np.float32)
 
 
+def shared_seed(net, rank):
+    """A seed every rank agrees on: rank 0 draws it from its own (possibly
+    user-seeded) global numpy stream, the host all-reduce hands it to the
+    others (which contribute 0)."""
+    seed = float(np.random.randint(0, 2 ** 31 - 1)) if rank == 0 else 0.0
+    return int(net.allreduce_host([seed])[0])
+
+
 def permutation_batches(n, batch_size):
     """Batch indices of fit's loop (models_att.py:193-200): a deque refilled
     with np.random.permutation(n) whenever fewer than batch_size indices
@@ -80,6 +95,7 @@ class base_model(object):
         self.checkpoints = "final"
         self.writer = None
         self._loss_ema = None
+        self._rank, self._world = 0, 1
 
     # ------------------------------------------------------------------ predict
     def predict(self, data, labels=None, sess=None):
@@ -92,10 +108,12 @@ class base_model(object):
         data = self._dense(data)
         size = data.shape[0]
         net.dataset_upload(_SLOT_PX, data)
-        if labels is None:
-            return net.predict_dataset(_SLOT_PX, size, self.batch_size)
-        net.dataset_upload(_SLOT_PL, np.asarray(labels).reshape(size, -1))
-        predictions, losses = net.predict_dataset(_SLOT_PX, size, self.batch_size, lab_slot=_SLOT_PL)
+        with self._rank_local(net):
+            if labels is None:
+                return net.predict_dataset(_SLOT_PX, size, self.batch_size)
+            net.dataset_upload(_SLOT_PL, np.asarray(labels).reshape(size, -1))
+            predictions, losses = net.predict_dataset(_SLOT_PX, size, self.batch_size,
+                                                      lab_slot=_SLOT_PL)
         return predictions, self._mean_batch_loss(losses, size)
 
     def predict_tta(self, data, flip=False, rotate=False, translation=None, sess=None):
@@ -107,7 +125,26 @@ class base_model(object):
         data = self._dense(data)
         aug, undo, _ = augment_ops(flip=flip, rotate=rotate, translation=translation)
         net.dataset_upload(_SLOT_PX, data)
-        return net.predict_dataset(_SLOT_PX, data.shape[0], self.batch_size, augment=aug, undo=undo)
+        with self._rank_local(net):
+            return net.predict_dataset(_SLOT_PX, data.shape[0], self.batch_size, augment=aug,
+                                       undo=undo)
+
+    def _rank_local(self, net):
+        """predict's batches are the reference's fixed batch_size batches with
+        their own BN statistics (models_att.py:88-121): with several ranks every
+        rank runs them whole, without exchanges, and gets the same result."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def ctx():
+            if self._world > 1:
+                net.comm_suspend(True)
+            try:
+                yield
+            finally:
+                if self._world > 1:
+                    net.comm_suspend(False)
+        return ctx()
 
     @staticmethod
     def _dense(data):
@@ -124,7 +161,8 @@ class base_model(object):
 
     def _evaluate_resident(self, size, net):
         """evaluate() on the validation set already in HBM (fit's eval step)."""
-        _, losses = net.predict_dataset(_SLOT_VX, size, self.batch_size, lab_slot=_SLOT_VL)
+        with self._rank_local(net):
+            _, losses = net.predict_dataset(_SLOT_VX, size, self.batch_size, lab_slot=_SLOT_VL)
         loss = self._mean_batch_loss(losses, size)
         return "loss: {:.4e}".format(loss), loss
 
@@ -144,11 +182,15 @@ class base_model(object):
         t_process, t_wall = time.process_time(), time.time()
         starting_step = 1
         net = self._net
+        rank, world = self._rank, self._world
+        lead = rank == 0          # the rank that prints and writes files
+        say = print if lead else (lambda *a, **k: None)
         path = os.path.join(self._get_path("checkpoints"), "final", "model")
         best_path = os.path.join(self._get_path("checkpoints"), "best", "model")
         if starting_checkpoint is None:
-            shutil.rmtree(self._get_path("checkpoints"), ignore_errors=True)
-            os.makedirs(self._get_path("checkpoints"))
+            if lead:
+                shutil.rmtree(self._get_path("checkpoints"), ignore_errors=True)
+                os.makedirs(self._get_path("checkpoints"))
             self._initialize()
         else:
             found = None
@@ -159,8 +201,8 @@ class base_model(object):
             if found is None:
                 raise FileNotFoundError(f"no model-<step> checkpoint in {starting_checkpoint}")
             starting_step = found
-            print(f"Resuming from step {starting_step}")
-            print(f"Restoring from checkpoint: {starting_checkpoint}")
+            say(f"Resuming from step {starting_step}")
+            say(f"Restoring from checkpoint: {starting_checkpoint}")
             ema = ckpt.restore(net, ckpt.latest_checkpoint(starting_checkpoint))
             if ema is not None:
                 self._loss_ema = list(ema)
@@ -170,7 +212,12 @@ class base_model(object):
         # counter-based generator, seeded outside numpy's global stream so the
         # batch permutations stay the reference's draws
         seed = int(os.environ.get("LCN_DROPOUT_SEED", int.from_bytes(os.urandom(8), "little")))
+        if world > 1:  # one mask stream for the whole batch: rank 0's seed (53 bits survive the double)
+            seed = int(net.allreduce_host([float(seed % 2 ** 53) if lead else 0.0])[0])
+            # every rank draws the same batch permutations from here on
+            np.random.seed(shared_seed(net, rank))
         net.set_dropout(float(self.dropout or 0.0), seed)
+        shard = dist.shard_slice(self.batch_size, world, rank)
         losses = []
         # the deque of np.random.permutation() indices of :193-200, kept as an
         # array (same draws, same order); the arrays themselves live in HBM
@@ -181,59 +228,64 @@ class base_model(object):
         net.dataset_upload(_SLOT_VL, np.asarray(val_labels).reshape(val_data.shape[0], -1))
         num_steps = int(self.num_epochs * train_data.shape[0] / self.batch_size)
         eval_frequency = max(1, num_steps // self.num_epochs)
-        print(f"Total steps to be done to complete all the epochs: {num_steps}")
+        say(f"Total steps to be done to complete all the epochs: {num_steps}")
         min_loss = 10000
         training_error, validation_error = [], []
         loss_average = float("nan")
         for step in range(starting_step, num_steps + 1):
-            idx = next(batches)
+            idx = next(batches)[shard]  # every rank draws the batch, steps its shard
             loss, learning_rate = net.train_step_indexed(_SLOT_TX, _SLOT_TL, idx)
             loss_average = self._update_loss_average(loss)
 
             if step % eval_frequency == 0:
                 epoch = step * self.batch_size / train_data.shape[0]
-                print("step {} / {} (epoch {:.2f} / {}):".format(step, num_steps, epoch,
-                                                                 self.num_epochs))
-                print("  learning_rate = {:.2e}, loss_average = {:.4e}".format(learning_rate,
-                                                                               loss_average))
+                say("step {} / {} (epoch {:.2f} / {}):".format(step, num_steps, epoch,
+                                                               self.num_epochs))
+                say("  learning_rate = {:.2e}, loss_average = {:.4e}".format(learning_rate,
+                                                                             loss_average))
                 training_error.append([time.time(), step, float(loss_average)])
                 string, loss = self._evaluate_resident(val_data.shape[0], net)
                 losses.append(loss)
-                print("validation {}".format(string))
-                print("time: {:.0f}s (wall {:.0f}s)".format(time.process_time() - t_process,
-                                                           time.time() - t_wall))
+                say("validation {}".format(string))
+                say("time: {:.0f}s (wall {:.0f}s)".format(time.process_time() - t_process,
+                                                         time.time() - t_wall))
                 validation_error.append([0, step, float(loss)])
-                self._write_summary(step, learning_rate, loss_average, loss)
-                ckpt.save(net, path, step, self._ckpt_meta(), self._loss_ema)
+                if lead:
+                    self._write_summary(step, learning_rate, loss_average, loss)
+                    ckpt.save(net, path, step, self._ckpt_meta(), self._loss_ema)
                 if loss < min_loss:
                     min_loss = loss
-                    ckpt.save(net, best_path, step, self._ckpt_meta(), self._loss_ema)
+                    if lead:
+                        ckpt.save(net, best_path, step, self._ckpt_meta(), self._loss_ema)
 
-        print("validation loss: trough = {:.4f}, mean = {:.2f}".format(
+        say("validation loss: trough = {:.4f}, mean = {:.2f}".format(
             min_loss, np.mean(losses[-10:]) if losses else float("nan")))
         t_step = (time.time() - t_wall) / max(num_steps, 1)
-        if output_dir is not None:
+        if world > 1:
+            net.allreduce_host([0.0])  # rank 0's files are complete when any rank returns
+        if output_dir is not None and lead:
             os.makedirs(output_dir, exist_ok=True)
             with open(output_dir + "/training_error.json", "w") as f:
                 f.write(json.dumps([training_error], indent=4))
             with open(output_dir + "/validation_error.json", "w") as f:
                 f.write(json.dumps([validation_error], indent=4))
         if training_error:
-            print("Final training error: ", training_error[-1])
-            print("Final validation error: ", validation_error[-1])
+            say("Final training error: ", training_error[-1])
+            say("Final validation error: ", validation_error[-1])
         return losses, t_step
 
     # ----------------------------------------------------------------- helpers
     def _update_loss_average(self, loss):
-        """tf.train.ExponentialMovingAverage(0.9) of a tensor: zero-debiased
-        (models_att.py:370-379)."""
+        """tf.compat.v1.train.ExponentialMovingAverage(0.9) applied to the loss
+        tensor (models_att.py:370-379): the shadow starts at 0 and, zero_debias
+        being off by default, is reported as it is -- the first tens of steps
+        read low, exactly as the reference's loss_average does."""
         if self._loss_ema is None:
             self._loss_ema = [0.0, 0]
-        biased, n = self._loss_ema
-        biased = 0.9 * biased + 0.1 * float(loss)
-        n += 1
-        self._loss_ema = [biased, n]
-        return biased / (1 - 0.9 ** n)
+        shadow, n = self._loss_ema
+        shadow = 0.9 * shadow + 0.1 * float(loss)
+        self._loss_ema = [shadow, n + 1]
+        return shadow
 
     def _write_summary(self, step, lr, loss_average, val_loss):
         d = self._get_path("summaries")
@@ -258,9 +310,10 @@ class base_model(object):
         """sess=None: restore the latest <checkpoints> checkpoint (models_att.py:445-463)."""
         if sess is not None:
             return sess
-        print(self._get_path("checkpoints"))
         filename = ckpt.latest_checkpoint(os.path.join(self._get_path("checkpoints"), self.checkpoints))
-        print("restore from %s" % filename)
+        if self._rank == 0:
+            print(self._get_path("checkpoints"))
+            print("restore from %s" % filename)
         if filename is None:
             raise FileNotFoundError("no checkpoint under " + self._get_path("checkpoints"))
         ckpt.restore(self._net, filename)
@@ -299,15 +352,23 @@ class cgcnn(base_model):
         if self.decay_type != "exp":
             raise AssertionError("not implemented lr decay types!")
         dp = self.decay_params or {"decay_steps": 32000, "decay_rate": 0.96}
+        rank, world, local = dist.dist_env()
+        self._rank, self._world = rank, world
         self._net = Network(F=self.F, in_F=in_F, num_layers=self.num_layers,
                             mask_type=self.mask_type, mask_matrix=self._mask_matrix,
                             residual=self.residual, batch_norm=self.batch_norm,
                             max_norm=self.max_norm, regularization=self.regularization,
                             learning_rate=self.learning_rate, decay_steps=dp["decay_steps"],
                             decay_rate=dp["decay_rate"], max_batch=self.batch_size,
-                            device=int(os.environ.get("LOCAL_RANK", "0")))
+                            device=local)
+        if world > 1:
+            # one process per GPU: RCCL communicator over the node's ranks; a
+            # training step is then data parallel over each rank's shard
+            if self.batch_size < world:
+                raise ValueError(f"batch_size {self.batch_size} < {world} ranks")
+            dist.comm_setup(self._net, rank, world)
         self._initialize()
-        if os.path.exists(self._get_path("summaries")):
+        if rank == 0 and os.path.exists(self._get_path("summaries")):
             shutil.rmtree(self._get_path("summaries"))
 
     def initialize_mask(self):
@@ -324,7 +385,12 @@ class cgcnn(base_model):
             self._mask_matrix = get_exponential_matrix()
 
     def _initialize(self):
-        flat = init_flat(self._net.param_layout(), self._net.n_params, self.neighbour_matrix)
+        # every replica starts from the same draw; LCN_INIT_SEED pins it (tests)
+        if os.environ.get("LCN_INIT_SEED") is not None:
+            seed = int(os.environ["LCN_INIT_SEED"])
+        else:
+            seed = shared_seed(self._net, self._rank) if self._world > 1 else None
+        flat = init_flat(self._net.param_layout(), self._net.n_params, self.neighbour_matrix, seed=seed)
         self._net.set_params(flat)
         n = self._net.n_params
         self._net.set_optimizer_state(np.zeros(n, np.float32), np.zeros(n, np.float32), 0, 0.9, 0.999)

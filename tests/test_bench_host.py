@@ -79,5 +79,76 @@ def test_claim_stdout_keeps_the_result_line_apart(capfd):
     assert "RCCL version" in captured.err
 
 
+RANK_STUB = """
+import json, os, sys, time
+out = os.environ["STUB_OUT"]
+rec = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+rec["argv"] = sys.argv[1:]
+with open(os.path.join(out, "rank%s.json" % rec["RANK"]), "w") as f:
+    json.dump(rec, f)
+if os.environ.get("STUB_FAIL_RANK") == rec["RANK"]:
+    sys.exit(3)
+if os.environ.get("STUB_FAIL_RANK") is not None:
+    time.sleep(60)   # the surviving ranks would wait in a collective
+if rec["RANK"] == "0":
+    print(json.dumps({"n_gpus": int(rec["WORLD_SIZE"])}))
+"""
+
+
+def _spawn(tmp_path, monkeypatch, n, fail_rank=None):
+    stub = tmp_path / "rank_stub.py"
+    stub.write_text(RANK_STUB)
+    monkeypatch.setenv("STUB_OUT", str(tmp_path))
+    if fail_rank is not None:
+        monkeypatch.setenv("STUB_FAIL_RANK", str(fail_rank))
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    argv = ["--gpus", str(n), "--steps", "2"]
+    return bench.spawn_ranks(bench.parse(argv), argv, script=str(stub))
+
+
+def test_gpus_n_starts_n_ranks_with_their_environment(tmp_path, monkeypatch, capfd):
+    import json
+    assert _spawn(tmp_path, monkeypatch, 4) == 0
+    recs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(4)]
+    assert [r["RANK"] for r in recs] == ["0", "1", "2", "3"]
+    assert [r["LOCAL_RANK"] for r in recs] == ["0", "1", "2", "3"]
+    assert {r["WORLD_SIZE"] for r in recs} == {"4"} and {r["MASTER_ADDR"] for r in recs} == {"127.0.0.1"}
+    assert len({r["MASTER_PORT"] for r in recs}) == 1
+    assert all(r["argv"] == ["--gpus", "4", "--steps", "2"] for r in recs)
+    # rank 0's line is the command's stdout
+    assert json.loads(capfd.readouterr().out.strip())["n_gpus"] == 4
+
+
+def test_a_failing_rank_fails_the_run_and_stops_the_others(tmp_path, monkeypatch):
+    import time
+    t0 = time.time()
+    assert _spawn(tmp_path, monkeypatch, 3, fail_rank=1) != 0
+    assert time.time() - t0 < 30   # the other ranks were stopped, not waited for
+
+
+def test_world_size_must_match_gpus(monkeypatch, capsys):
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "0")
+    assert bench.main(["--gpus", "4"]) == 2
+    assert "WORLD_SIZE=2" in capsys.readouterr().err
+
+
+def test_batch_plan_strong_and_weak():
+    a = bench.parse([])
+    assert a.global_batch == 65536 and a.mode == "train" and (a.knn, a.layers, a.channels) == (3, 3, 64)
+    rows = [bench.batch_plan(a, 8, r) for r in range(8)]
+    assert rows == [(8192, 65536, "strong")] * 8
+    a = bench.parse(["--global-batch", "1000"])
+    assert [bench.batch_plan(a, 3, r)[0] for r in range(3)] == [334, 333, 333]
+    a = bench.parse(["--batch", "4096"])
+    assert bench.batch_plan(a, 4, 2) == (4096, 16384, "weak")
+    a = bench.parse(["--config", "cfg4"])
+    assert (a.mask_type, a.layers, a.channels, a.global_batch) == ("exponential", 6, 256, 131072)
+    a = bench.parse(["--config", "cfg5"])
+    assert a.mode == "predict" and a.knn == 5 and a.global_batch == 262144
+    with pytest.raises(SystemExit):
+        bench.parse(["--batch", "64", "--global-batch", "128"])
+
+
 if __name__ == "__main__":
     sys.exit(pytest.main([__file__, "-q"]))

@@ -88,3 +88,57 @@ def test_augmentation_helpers_match_reference(golden_dir):
     np.testing.assert_allclose(data.rotate_data(g["rot_in3"], 90), g["rot_out3_90"], atol=1e-12)
     np.testing.assert_allclose(data.undo(g["undo_in"], {"f": 1, "r": 2, "t": 3}, 3, translation=0.05),
                                g["undo_out_frt"], atol=1e-12)
+
+
+# ---- one process per GPU: batch shards and shared seeds (lcn_amd/dist.py, cgcnn.fit) ----
+def test_batch_shards_tile_the_batch():
+    from lcn_amd import dist
+    for total, world in ((200, 8), (512, 3), (65536, 8), (7, 7), (10, 4)):
+        sl = [dist.shard_slice(total, world, r) for r in range(world)]
+        assert sl[0].start == 0 and sl[-1].stop == total
+        assert all(a.stop == b.start for a, b in zip(sl, sl[1:]))          # contiguous, in rank order
+        sizes = [s.stop - s.start for s in sl]
+        assert sizes == [dist.shard_rows(total, world, r) for r in range(world)]
+        assert max(sizes) - min(sizes) <= 1
+    # the ranks' slices of one drawn batch are exactly that batch, in order
+    idx = np.random.permutation(1000)[:200]
+    parts = [idx[dist.shard_slice(200, 3, r)] for r in range(3)]
+    np.testing.assert_array_equal(np.concatenate(parts), idx)
+
+
+class _SeedNet:
+    """allreduce_host over fake ranks: sums what every rank contributes."""
+    def __init__(self, contributions):
+        self.contrib = contributions
+
+    def allreduce_host(self, values, op="sum"):
+        self.contrib.append(float(values[0]))
+        return np.asarray([sum(self.contrib)])
+
+
+def test_every_rank_draws_rank0s_seed_and_the_same_permutations():
+    from network import models_att
+    np.random.seed(123)
+    expect = int(np.random.randint(0, 2 ** 31 - 1))
+    np.random.seed(123)
+    box = []
+    s0 = models_att.shared_seed(_SeedNet(box), rank=0)        # rank 0 contributes its draw
+    s1 = models_att.shared_seed(_SeedNet(box), rank=1)        # the others contribute 0
+    assert s0 == s1 == expect
+    draws = []
+    for _ in range(2):                                         # two "ranks" reseed alike
+        np.random.seed(s0)
+        g = models_att.permutation_batches(50, 20)
+        draws.append([next(g).copy() for _ in range(4)])
+    for a, b in zip(*draws):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_env_overrides_pick_device_and_transport(monkeypatch):
+    from lcn_amd import dist
+    monkeypatch.setenv("RANK", "3")
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    assert dist.dist_env() == (3, 4, 3)
+    monkeypatch.setenv("LCN_DEVICE", "0")
+    assert dist.dist_env() == (3, 4, 0)
