@@ -217,6 +217,19 @@ int lcn_comm_allreduce_host(void* handle, double* values, int32_t count, int32_t
 int lcn_eval_mpjpe(int32_t device, int64_t n, const double* pred, const double* gt, const double* box,
                    const double* cam, const double* root_depth, int32_t protocol2, double* err);
 
+/* lcn_eval_mpjpe for callers that cannot allocate device memory (harnesses
+ * that forbid hipMalloc, tight evaluation loops): same arguments, results
+ * and errors, but the host arrays are staged in a fixed per-GPU array of the
+ * library (LCN_EVAL_STATIC_MAX_FRAMES frames, 1 KiB each; every GPU the
+ * library runs on holds it until the process ends) on the null stream, so the
+ * call makes no hipMalloc / hipFree / stream creation.  n beyond the limit is
+ * LCN_E_ARG.  Calls that overlap on one GPU race on that array: serialise
+ * them.  Errors: lcn_last_error(NULL).  No counterpart in the reference. */
+#define LCN_EVAL_STATIC_MAX_FRAMES 16384
+int lcn_eval_mpjpe_static(int32_t device, int64_t n, const double* pred, const double* gt,
+                          const double* box, const double* cam, const double* root_depth,
+                          int32_t protocol2, double* err);
+
 /* --- checkpoint I/O helpers (host only) -------------------------------- */
 /* CRC-32C of TensorFlow tensor-bundle checkpoints (tf.train.Saver files the
  * reference writes and restores, models_att.py:256-260, 321-322, 457-461):

@@ -162,3 +162,106 @@ void launch_mpjpe(int64_t n, const double* pred, const double* gt, const double*
 }
 
 }  // namespace lcn
+
+// ---------------------------------------------------------------------------
+// lcn_eval_mpjpe_static: lcn_eval_mpjpe for callers that must not allocate.
+//
+// lcn_eval_mpjpe stages the host arrays in device buffers it allocates (and
+// frees) per call, on a stream it creates.  This variant stages them in a
+// fixed array of the code object instead -- `scratch`, one copy per GPU, held
+// until the process ends -- and uses the null stream: no hipMalloc, hipFree or
+// stream creation, at the price of a frame limit (kStaticMaxFrames per call).
+// Every call on a GPU shares that GPU's array: overlapping calls on one GPU
+// race (serialise them); nothing in it has to start at zero, each call
+// overwrites the part it reads.
+// ---------------------------------------------------------------------------
+#include <mutex>
+#include <string>
+
+#include "../../include/lcn.h"
+
+namespace {
+
+constexpr int64_t kStaticMaxFrames = LCN_EVAL_STATIC_MAX_FRAMES;
+// per frame: pred 51 + gt 51 + box 4 + cam 4 + root_depth 1 + err 17 doubles
+constexpr int64_t kStaticDoublesPerFrame = 51 + 51 + 4 + 4 + 1 + 17;
+constexpr size_t kStaticBytes = (size_t)kStaticMaxFrames * kStaticDoublesPerFrame * sizeof(double);
+
+// In host code this name is only a handle for hipGetSymbolAddress: the
+// device address of each GPU's copy is looked up once and kept in
+// g_static_ptr; host code passes that pointer, never the array.
+static __device__ __align__(256) unsigned char scratch[kStaticBytes];
+
+constexpr int kMaxDevices = 64;
+std::mutex g_static_mu;
+double* g_static_ptr[kMaxDevices];      // per device, null until looked up
+// errors are reported like lcn_eval_mpjpe's: lcn_last_error(NULL)
+struct StaticError {
+  StaticError& operator=(const std::string& m) { lcn::set_global_error(m); return *this; }
+  void clear() { lcn::set_global_error(""); }
+} g_static_error;
+
+// the device address of `device`'s copy of the scratch array (device current)
+int static_scratch(int device, double** out) {
+  std::lock_guard<std::mutex> lock(g_static_mu);
+  if (!g_static_ptr[device]) {
+    void* p = nullptr;
+    const hipError_t e = hipGetSymbolAddress(&p, HIP_SYMBOL(scratch));
+    if (e != hipSuccess || !p) {
+      g_static_error = std::string("lcn_eval_mpjpe_static: hipGetSymbolAddress: ") + hipGetErrorString(e);
+      return LCN_E_HIP;
+    }
+    g_static_ptr[device] = (double*)p;
+  }
+  *out = g_static_ptr[device];
+  return LCN_OK;
+}
+
+}  // namespace
+
+extern "C" int lcn_eval_mpjpe_static(int32_t device, int64_t n, const double* pred, const double* gt,
+                                     const double* box, const double* cam, const double* root_depth,
+                                     int32_t protocol2, double* err) {
+  g_static_error.clear();
+  if (device < 0 || device >= kMaxDevices) {
+    g_static_error = "lcn_eval_mpjpe_static: device must be in [0, 64)";
+    return LCN_E_ARG;
+  }
+  if (n < 0 || (n > 0 && (!pred || !gt || !box || !cam || !root_depth || !err))) {
+    g_static_error = "lcn_eval_mpjpe_static: null argument or negative frame count";
+    return LCN_E_ARG;
+  }
+  if (n > kStaticMaxFrames) {
+    g_static_error = "lcn_eval_mpjpe_static: " + std::to_string(n) + " frames exceed the static limit of " +
+                     std::to_string(kStaticMaxFrames) + " per call (split the frames, or use lcn_eval_mpjpe)";
+    return LCN_E_ARG;
+  }
+  if (n == 0) return LCN_OK;
+  auto fail = [](const char* what, hipError_t e) {
+    g_static_error = std::string("lcn_eval_mpjpe_static: ") + what + ": " + hipGetErrorString(e);
+    return LCN_E_HIP;
+  };
+  hipError_t e;
+  if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
+  double* base = nullptr;
+  const int rc = static_scratch(device, &base);
+  if (rc != LCN_OK) return rc;
+  // sub-arrays at fixed offsets (sized for the frame limit; all multiples of 256 B)
+  double* d_pred = base;
+  double* d_gt = d_pred + kStaticMaxFrames * 51;
+  double* d_box = d_gt + kStaticMaxFrames * 51;
+  double* d_cam = d_box + kStaticMaxFrames * 4;
+  double* d_root = d_cam + kStaticMaxFrames * 4;
+  double* d_err = d_root + kStaticMaxFrames;
+  const size_t f = (size_t)n * sizeof(double);
+  if ((e = hipMemcpy(d_pred, pred, f * 51, hipMemcpyHostToDevice)) != hipSuccess) return fail("copy pred", e);
+  if ((e = hipMemcpy(d_gt, gt, f * 51, hipMemcpyHostToDevice)) != hipSuccess) return fail("copy gt", e);
+  if ((e = hipMemcpy(d_box, box, f * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail("copy box", e);
+  if ((e = hipMemcpy(d_cam, cam, f * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail("copy cam", e);
+  if ((e = hipMemcpy(d_root, root_depth, f, hipMemcpyHostToDevice)) != hipSuccess) return fail("copy root_depth", e);
+  lcn::launch_mpjpe(n, d_pred, d_gt, d_box, d_cam, d_root, protocol2 ? 1 : 0, d_err, nullptr);
+  if ((e = hipGetLastError()) != hipSuccess) return fail("launch", e);
+  // the blocking copy on the null stream waits for the kernel
+  if ((e = hipMemcpy(err, d_err, f * lcn::kJ, hipMemcpyDeviceToHost)) != hipSuccess) return fail("copy out", e);
+  return LCN_OK;
+}

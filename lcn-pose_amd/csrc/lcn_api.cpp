@@ -165,6 +165,10 @@ struct Handle {
   std::vector<void*> allocs;
 };
 
+}  // namespace
+void lcn::set_global_error(const std::string& msg) { g_create_error = msg; }
+namespace {
+
 #define HIPC(expr)                                                                   \
   do {                                                                               \
     hipError_t e_ = (expr);                                                          \

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace lcn {
 
 constexpr int kJ = 17;          // joints (models_att.py:512-513)
@@ -209,6 +211,10 @@ void launch_rows_finish(const double* rows, int world, int rank, RowInfo* ri, hi
 // box [n][4], cam [n][4] = (cx, cy, fx, fy), root_depth [n] -> err [n][17]
 void launch_mpjpe(int64_t n, const double* pred, const double* gt, const double* box, const double* cam,
                   const double* root_depth, int protocol2, double* err, hipStream_t s);
+
+// message of a failed handle-free entry point, returned by lcn_last_error(NULL)
+// (per thread; lcn_api.cpp)
+void set_global_error(const std::string& msg);
 
 // ----------------------------------------------------------------------------
 // BatchNorm (batch statistics), activation, BN backward

@@ -90,6 +90,7 @@ SIGNATURES = {
     "lcn_crc32c": ([ctypes.c_uint32, ctypes.c_char_p, _i64], ctypes.c_uint32),
     "lcn_set_dropout": ([_vp, ctypes.c_float, ctypes.c_uint64], _i32),
     "lcn_eval_mpjpe": ([_i32, _i64, _f64p, _f64p, _f64p, _f64p, _f64p, _i32, _f64p], _i32),
+    "lcn_eval_mpjpe_static": ([_i32, _i64, _f64p, _f64p, _f64p, _f64p, _f64p, _i32, _f64p], _i32),
     "lcn_set_timing": ([_vp, _i32], _i32),
     "lcn_kernel_timing": ([_vp, _i32, _i64p, _f64p, _f64p], _i32),
     "lcn_debug_tensor": ([_vp, _i32, _i32, _f32p, _i64], _i32),
@@ -127,13 +128,18 @@ def load_library(path: Optional[str] = None):
     return lib
 
 
-def eval_mpjpe(pred, gt, box, cam, root_depth, protocol2: bool = False, device: int = 0) -> np.ndarray:
+EVAL_STATIC_MAX_FRAMES = 16384
+
+
+def eval_mpjpe(pred, gt, box, cam, root_depth, protocol2: bool = False, device: int = 0,
+               static: bool = False) -> np.ndarray:
     """Per-frame, per-joint camera-space error of evaluate.py's loop
     (evaluate.py:53-73) in one device launch (lcn_eval_mpjpe).
 
     pred [N, 17, 3] image-frame predictions, gt [N, 17, 3] joint_3d_camera,
     box [N, 4], cam [N, 4] = (cx, cy, fx, fy), root_depth [N]; all float64.
-    Returns err [N, 17] float64."""
+    Returns err [N, 17] float64.  static=True: the allocation-free entry point
+    (lcn_eval_mpjpe_static, at most EVAL_STATIC_MAX_FRAMES frames per call)."""
     lib = load_library()
     arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (pred, gt, box, cam, root_depth)]
     n = arrs[0].shape[0]
@@ -143,6 +149,12 @@ def eval_mpjpe(pred, gt, box, cam, root_depth, protocol2: bool = False, device: 
             raise ValueError(f"{name} has shape {a.shape}, expected {shp}")
     err = np.empty((n, 17), np.float64)
     ptr = [a.ctypes.data_as(_f64p) for a in arrs]
+    if static:
+        rc = lib.lcn_eval_mpjpe_static(device, n, *ptr, 1 if protocol2 else 0, err.ctypes.data_as(_f64p))
+        if rc != 0:
+            raise LcnNativeError(f"lcn_eval_mpjpe_static failed ({rc}): "
+                                 f"{lib.lcn_last_error(None).decode()}")
+        return err
     rc = lib.lcn_eval_mpjpe(device, n, *ptr, 1 if protocol2 else 0, err.ctypes.data_as(_f64p))
     if rc != 0:
         raise LcnNativeError(f"lcn_eval_mpjpe failed ({rc}): {lib.lcn_last_error(None).decode()}")
