@@ -123,6 +123,30 @@ def test_duplicated_batch_gives_same_gradients():
         assert rel_err(g2[off:off + n], g1[off:off + n]) < 1e-4, name
 
 
+def test_duplicated_batch_gives_same_gradients_cfg4_shape():
+    """The same property at BASELINE.json configs[3]'s model shape (dense
+    exponential mask, F 256, 6 blocks, H 4352) and its per-GPU batch on 8
+    GPUs: 8 192 poses -> 16 384.  BN-parameter gradients at this shape are
+    sums with heavy cancellation, hence the looser bar for them; a wrong
+    batch reduction (a dropped tile, a wrong count) is off by far more."""
+    cfg = make_cfg(F=256, L=6, knn=2, mask="exponential")
+    params = perturbed_params(cfg)
+    x, lab = synthetic_batch(8192, 2, seed=5)
+    net = make_network(cfg, max_batch=16384)
+    net.set_params(O.flatten(cfg, params))
+    l1, _ = net.train_step(x, lab, update=False, keep_grads=True)
+    g1 = net.get_grads()
+    l2, _ = net.train_step(np.concatenate([x, x]), np.concatenate([lab, lab]), update=False,
+                           keep_grads=True)
+    g2 = net.get_grads()
+    assert l2 == pytest.approx(l1, rel=1e-6)
+    for name, off, shape in net.param_layout():
+        n = int(np.prod(shape))
+        tol = 1e-3 if name.endswith(("_gamma", "_beta")) else 1e-4
+        assert rel_err(g2[off:off + n], g1[off:off + n]) < tol, name
+    net.close()
+
+
 def test_phased_reductions_match_single_pass(monkeypatch):
     """The multi-GPU reduction path (per-rank phase-1 sums -> all-reduce ->
     phase-2 finish, lcn_api.cpp bn_stats / bn_back) forced on one GPU, where
