@@ -3,6 +3,7 @@
 // Build: make gemm_bench ; run: ./gemm_bench [B] [iters]
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -98,10 +99,19 @@ int main(int argc, char** argv) {
   int* dbp = dev(bptr);
   int2* dfi = dev(fidx);
   int2* dbi = dev(bidx);
+  auto by_length = [&](const std::vector<int>& ptr) {
+    std::vector<int> o(J);
+    for (int i = 0; i < J; ++i) o[i] = i;
+    std::stable_sort(o.begin(), o.end(), [&](int x, int y) { return ptr[x + 1] - ptr[x] > ptr[y + 1] - ptr[y]; });
+    return o;
+  };
+  int* dfo = dev(by_length(fptr));
+  int* dbo = dev(by_length(bptr));
+  const int tail = std::getenv("LCN_GEMM_TAIL") ? std::atoi(std::getenv("LCN_GEMM_TAIL")) : 16;
   float* Y;
   CK(hipMalloc(&Y, (size_t)B * H * 4));
   float2* stat;
-  CK(hipMalloc(&stat, (size_t)(B / 32 + 1) * H * 8));
+  CK(hipMalloc(&stat, (size_t)(B / 32 + 1) * H * 8 + (size_t)B * 17));
   const int nch = std::max(1, std::min(64, 8192 / nblk));
   float* part;
   CK(hipMalloc(&part, (size_t)nch * nblk * 4096 * 4));
@@ -125,6 +135,8 @@ int main(int argc, char** argv) {
     a.blocks = W;
     a.ptr = fwd ? dfp : dbp;
     a.idx = fwd ? dfi : dbi;
+    a.order = tail > 0 ? (fwd ? dfo : dbo) : nullptr;
+    a.tail = tail;
     a.bias = fwd ? bias : nullptr;
     a.pro_mode = pro;
     a.pro_scale = pro ? sc : nullptr;
@@ -228,6 +240,41 @@ int main(int argc, char** argv) {
                   ms * 1e3, flop / (ms * 1e-3) / 1e12, 100.0 * flop / (ms * 1e-3) / 1e12 / 157.3);
     }
   }
+#ifdef EXP_CLOCK
+  {  // in-kernel clock of the no-epilogue forward GEMM after sustained load,
+     // and the occupancy profile of its last launch (how long the tail is)
+    GemmArgs a = mk(3, PRO_RAW, 0);
+    const int grid = 8 * (((a.n_rt + kGemmWaves - 1) / kGemmWaves + 7) / 8) * a.n_out_slabs;
+    for (int it = 0; it < 1500; ++it) launch_gemm_bs(a, s);   // > 1 s of back-to-back launches
+    CK(hipStreamSynchronize(s));
+    std::vector<uint64_t> st((size_t)4 * grid);
+    CK(hipMemcpy(st.data(), stat, st.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<double> ghz;
+    uint64_t t0 = ~0ull, t1 = 0;
+    for (int i = 0; i < grid; ++i) {
+      if (st[4 * i + 1] > 100) ghz.push_back((double)st[4 * i] / (double)st[4 * i + 1] * 0.1);
+      t0 = std::min(t0, st[4 * i + 2]);
+      t1 = std::max(t1, st[4 * i + 3]);
+    }
+    std::sort(ghz.begin(), ghz.end());
+    std::printf("in-kernel clock (GHz) over %zu workgroups: min %.3f median %.3f max %.3f\n", ghz.size(),
+                ghz.front(), ghz[ghz.size() / 2], ghz.back());
+    // resident workgroups over time, in 20 bins of the launch
+    const double span = (double)(t1 - t0);
+    std::vector<double> act(20, 0.0);
+    double wsum = 0;
+    for (int i = 0; i < grid; ++i) {
+      const double b0 = (st[4 * i + 2] - t0) / span * 20, b1 = (st[4 * i + 3] - t0) / span * 20;
+      wsum += (double)(st[4 * i + 3] - st[4 * i + 2]);
+      for (int b = (int)b0; b < 20 && b <= (int)b1; ++b)
+        act[b] += std::min(b1, (double)b + 1) - std::max(b0, (double)b);
+    }
+    std::printf("launch span %.1f us, mean workgroup life %.1f us; resident workgroups per 5%% bin:", span * 0.01,
+                wsum / grid * 0.01);
+    for (double v : act) std::printf(" %.0f", v);
+    std::printf("\n");
+  }
+#endif
   CK(hipGetLastError());
   return 0;
 }

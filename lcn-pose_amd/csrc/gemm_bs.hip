@@ -103,8 +103,35 @@ constexpr int kEpiBnBackDrop = 3;
 template <int PRO, int EPI>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gemm_bs_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) float4 Wl[];  // [2][1024] (+ BN tables)
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int rtg = wg / a.n_out_slabs, so = wg - rtg * a.n_out_slabs;
+#ifdef EXP_CLOCK
+  // diagnostic build: shader-clock and 100 MHz real-time stamps around the
+  // workgroup, written to a buffer of their own (a.stat is unused by EPI_NONE)
+  const uint64_t ck0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  // Work map.  Workgroups b, b + 8, ... share an XCD (and its L2): each XCD
+  // takes a contiguous range of row-tile groups and walks it group by group,
+  // so the ~10 output slabs that read an input slab run close in time.  The
+  // lists differ in length (5..17 slabs at knn 3) and a workgroup lives ~10 %
+  // of the launch, so in natural order the launch ends in a long drain; the
+  // last `tail` groups of each XCD are therefore issued longest list first
+  // across those groups (order[]): what is still running at the end is short.
+  const int nso = a.n_out_slabs;
+  const int n_rtg = (a.n_rt + kGemmWaves - 1) / kGemmWaves;
+  const int xcd = blockIdx.x & 7, li = blockIdx.x >> 3;
+  const int per = (n_rtg + 7) >> 3;
+  const int g0 = xcd * per, R = min(per, n_rtg - g0);
+  if (R <= 0 || li >= R * nso) return;  // padding of the grid (uniform per workgroup)
+  const int T = a.order ? min(R, a.tail) : 0;
+  int rtg, so;
+  if (li < (R - T) * nso) {
+    rtg = li / nso;
+    so = li - rtg * nso;
+    rtg += g0;
+  } else {
+    const int j = li - (R - T) * nso, rank = j / T;
+    so = a.order[rank];
+    rtg = g0 + (R - T) + (j - rank * T);
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int rt_raw = rtg * kGemmWaves + w;
   const bool live = rt_raw < a.n_rt;
@@ -124,7 +151,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   // bias / residual / table loads below are batched behind them, so the
   // prologue waits for memory once (not once per accumulator quarter)
   const int S_out = a.S_out, ncols = S_out * kSlab;
-  const size_t tbase = ((size_t)rt * S_out + so) * 512 + lane;  // float4 index of chunk 0
+  // float4 index of chunk 0 (fits 32 bits: max_batch * 17F <= INT32_MAX is checked at create)
+  const int tbase = (rt * S_out + so) * 512 + lane;
   DECLX(xa)
   DECLX(xb)
   int2 ia = idx[beg], ib = ia;
@@ -198,11 +226,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   }
 
   // ---- epilogue ----
+  // The tile index is rebuilt here instead of being carried through the loop
+  // (as a 64-bit address offset it cost the BN-apply instance two spilled
+  // registers); the empty asm keeps the compiler from reusing the earlier value.
+  int rt_e = rt;
+  asm volatile("" : "+v"(rt_e));
+  const int tbase_e = (rt_e * S_out + so) * 512 + lane;
   if constexpr (EPI == EPI_BNBACK || EPI == kEpiBnBackDrop) {
     // z of the layer below, issued before the output stores so its latency
     // overlaps them (keeping it live through the loop would cost 32 VGPRs,
     // i.e. a wave per SIMD of occupancy)
-    const float4* Z4 = (const float4*)a.epi_z + tbase;
+    const float4* Z4 = (const float4*)a.epi_z + tbase_e;
     zp0 = Z4[0]; zp1 = Z4[64]; zp2 = Z4[128]; zp3 = Z4[192];
     zp4 = Z4[256]; zp5 = Z4[320]; zp6 = Z4[384]; zp7 = Z4[448];
   }
@@ -213,17 +247,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
     float4* Y = (float4*)a.Y;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      Y[tbase + q * 64] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-      Y[tbase + (4 + q) * 64] =
+      Y[tbase_e + q * 64] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      Y[tbase_e + (4 + q) * 64] =
           make_float4(v[16 + 4 * q], v[16 + 4 * q + 1], v[16 + 4 * q + 2], v[16 + 4 * q + 3]);
     }
   }
+#ifdef EXP_CLOCK
+  if constexpr (EPI == EPI_NONE) {
+    if (threadIdx.x == 0 && a.stat) {
+      const uint64_t ck1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+      ((uint64_t*)a.stat)[4 * blockIdx.x] = ck1 - ck0;
+      ((uint64_t*)a.stat)[4 * blockIdx.x + 1] = rt1 - rt0;
+      ((uint64_t*)a.stat)[4 * blockIdx.x + 2] = rt0;
+      ((uint64_t*)a.stat)[4 * blockIdx.x + 3] = rt1;
+    }
+  }
+#endif
   if constexpr (EPI == EPI_NONE) return;
   // Column partials of the wave's 32x64 tile through its 8 KB of the (now
   // free) weight LDS: the wave writes float4 chunks with a lane swizzle
   // (position l ^ (2q + (l>>5)) of chunk q) that makes the column-wise reads
   // bank-conflict free; lane c then sums column c over the tile's rows.
   __syncthreads();  // all waves are done with the weight buffers
+  // Each wave transposes through its own 8 KB: a wave's LDS operations execute
+  // in issue order, so its column reads see its own writes (and a later write
+  // pass follows the earlier reads) without a workgroup barrier; the compiler
+  // only has to keep the program order.
+#define EPI_SYNC() __builtin_amdgcn_wave_barrier()
   float* red = (float*)Wl + w * 2048;
   const int c = lane, cg = c >> 3, chh = (c >> 2) & 1, cs = c & 3;
   const int n = live ? min(kRT, a.B - rt * kRT) : 0;  // valid rows of the tile
@@ -242,7 +292,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   if constexpr (EPI == EPI_BNFWD) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) put(q, v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-    __syncthreads();
+    EPI_SYNC();
     float sum = 0.f, mean = 0.f, m2 = 0.f;
     if (n == kRT) {  // full tile: 16 reads in flight at a time; / 32 is exact as * (1/32)
 #pragma unroll
@@ -321,9 +371,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
       v[4 * q + 3] = fmaf(z4.w, sc.w, sh.w) > 0.f ? v[4 * q + 3] : v[4 * q + 3] * al;      \
       put(q, v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);                          \
     }                                                                                      \
-    __syncthreads();                                                                       \
+    EPI_SYNC();                                                                            \
     P_ = colsum(n);                                                                        \
-    __syncthreads();                                                                       \
+    EPI_SYNC();                                                                            \
     _Pragma("unroll") for (int q = 0; q < 8; ++q) {                                        \
       const float4 z4 = zq[q];                                                             \
       const int ch = 8 * q + 4 * h;                                                        \
@@ -331,7 +381,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
       put(q, v[4 * q] * ((z4.x - mu.x) * rs.x), v[4 * q + 1] * ((z4.y - mu.y) * rs.y),     \
           v[4 * q + 2] * ((z4.z - mu.z) * rs.z), v[4 * q + 3] * ((z4.w - mu.w) * rs.w));   \
     }                                                                                      \
-    __syncthreads();                                                                       \
+    EPI_SYNC();                                                                            \
     Q_ = colsum(n);                                                                        \
   }
   // column c summed over the tile's n rows in row order (a full tile with
@@ -370,7 +420,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
 }
 
 void launch_gemm_bs(const GemmArgs& a, hipStream_t s) {
-  const int grid = ((a.n_rt + kGemmWaves - 1) / kGemmWaves) * a.n_out_slabs;
+  const int n_rtg = (a.n_rt + kGemmWaves - 1) / kGemmWaves;
+  const int grid = 8 * ((n_rtg + 7) / 8) * a.n_out_slabs;  // 8 XCDs x row-tile groups per XCD x slabs
   // weight double buffer; BN tables / epilogue constants and the 4-wave merge after it
   const size_t lds = 2 * 1024 * sizeof(float4);
   const size_t ldse = lds + (256 + 4 * 64 * 3) * sizeof(float);

@@ -11,8 +11,11 @@ namespace lcn {
 // One workgroup = a group of up to two 64x64 blocks (si0, so), (si1, so) x
 // one batch chunk; waves (bi, hp) = (w >> 1, w & 1) compute rows 32hp..+31 of
 // block bi against all 64 columns (two 32x32 accumulators), so the staged D
-// slab -- and its BN-backward rebuild -- serves both blocks.  One 32-row tile
-// per LDS stage.  Work ids are chunk-major so the groups of one chunk (same
+// slab -- and its BN-backward rebuild -- serves both blocks.  A group of one
+// block (the last of an output slab with an odd number of blocks) splits the
+// block four ways instead, wave (qh, hp) = (w >> 1, w & 1) computing rows
+// 32hp..+31 x columns 32qh..+31 in one accumulator: half the MFMAs per stage,
+// no idle wave.  One 32-row tile per LDS stage.  Work ids are chunk-major so the groups of one chunk (same
 // batch rows) run on one XCD and share the activation tiles through its L2.
 //
 // Staging: every thread loads 2 float4 of each operand's 8 KB row-tile slab
@@ -44,7 +47,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int lr = lane & 31, h = lane >> 5;
   const int bi = w >> 1, hp = w & 1;
-  const bool wave_live = bi == 0 || two;
   const int r0 = chunk * a.chunk_rows;
   const int r1 = min(a.B, r0 + a.chunk_rows);
   const bool writer = DBB && a.dz_out && grp.w;
@@ -157,8 +159,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
     // wave priority so the other waves' staging does not starve it
     if (base + kRT < r1) DW_GLOAD(base + kRT);
     __syncthreads();
-    if (wave_live) {
-      __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1);
+    if (two) {
       const float* Ap = As[bi] + (32 * hp + lr) * kDwLd + 4 * h;
       const float* D0 = Ds + lr * kDwLd + 4 * h;
       const float* D1 = Ds + (32 + lr) * kDwLd + 4 * h;
@@ -176,18 +178,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
         acc0 = MFMA32(av.w, d0.w, acc0);
         acc1 = MFMA32(av.w, d1.w, acc1);
       }
-      __builtin_amdgcn_s_setprio(0);
+    } else {  // one block: this wave's quarter (rows 32hp.., columns 32bi..)
+      const float* Ap = As[0] + (32 * hp + lr) * kDwLd + 4 * h;
+      const float* Dq = Ds + (32 * bi + lr) * kDwLd + 4 * h;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 av = *(const float4*)(Ap + 8 * g);
+        const float4 dv = *(const float4*)(Dq + 8 * g);
+        acc0 = MFMA32(av.x, dv.x, acc0);
+        acc0 = MFMA32(av.y, dv.y, acc0);
+        acc0 = MFMA32(av.z, dv.z, acc0);
+        acc0 = MFMA32(av.w, dv.w, acc0);
+      }
     }
+    __builtin_amdgcn_s_setprio(0);
   }
 #undef DW_GLOAD
 #undef DW_IX
-  if (!wave_live) return;
-  float* out = a.part + ((size_t)chunk * a.nblk + (bi ? b1 : b0)) * 4096;
+  if (two) {
+    float* out = a.part + ((size_t)chunk * a.nblk + (bi ? b1 : b0)) * 4096;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int p = 32 * hp + (k & 3) + 8 * (k >> 2) + 4 * h;
-    out[p * 64 + lr] = acc0[k];
-    out[p * 64 + 32 + lr] = acc1[k];
+    for (int k = 0; k < 16; ++k) {
+      const int p = 32 * hp + (k & 3) + 8 * (k >> 2) + 4 * h;
+      out[p * 64 + lr] = acc0[k];
+      out[p * 64 + 32 + lr] = acc1[k];
+    }
+  } else {
+    float* out = a.part + ((size_t)chunk * a.nblk + b0) * 4096 + 32 * bi;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int p = 32 * hp + (k & 3) + 8 * (k >> 2) + 4 * h;
+      out[p * 64 + lr] = acc0[k];
+    }
   }
 }
 

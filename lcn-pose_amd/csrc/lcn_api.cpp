@@ -70,6 +70,7 @@ struct Handle {
   // block structure of the hidden layers (64-granular slabs)
   int nblk = 0;
   int *fwd_ptr = nullptr, *bwd_ptr = nullptr;
+  int *fwd_order = nullptr, *bwd_order = nullptr;   // output slabs by falling list length
   int2 *fwd_idx = nullptr, *bwd_idx = nullptr, *blk = nullptr;
   int *thin_ptr = nullptr, *out_ptr = nullptr;                  // thin layers (padded slab)
   int2 *thin_idx = nullptr, *out_idx = nullptr, *lift_blk = nullptr, *out_blk = nullptr;
@@ -344,6 +345,15 @@ int build(Handle* h, const lcn_config* c) {
   CHECK(upload(h, &h->bwd_ptr, bptr));
   CHECK(upload(h, &h->fwd_idx, fidx));
   CHECK(upload(h, &h->bwd_idx, bidx));
+  // tail schedule of the block-sparse GEMMs: output slabs, longest list first
+  auto by_length = [&](const std::vector<int>& ptr) {
+    std::vector<int> o(h->nslab);
+    for (int i = 0; i < h->nslab; ++i) o[i] = i;
+    std::stable_sort(o.begin(), o.end(), [&](int x, int y) { return ptr[x + 1] - ptr[x] > ptr[y + 1] - ptr[y]; });
+    return o;
+  };
+  CHECK(upload(h, &h->fwd_order, by_length(fptr)));
+  CHECK(upload(h, &h->bwd_order, by_length(bptr)));
   for (int so = 0; so < h->nslab; ++so)
     if (fptr[so + 1] == fptr[so]) {
       h->err = "output joint " + std::to_string(so / h->spj) + " has no input joint in the mask";
@@ -632,7 +642,15 @@ struct GemmCall {
   float* Y; int S_out; const float* addsrc;
   int epi_mode; int epi_layer;
   int timer; double flops_per_row;
+  const int* order = nullptr;   // tail schedule (hidden layers); null: natural order
 };
+
+// row-tile groups per XCD issued longest-list-first at the end of a launch
+// (LCN_GEMM_TAIL overrides, 0 = natural order throughout)
+int tail_groups() {
+  static const int t = std::getenv("LCN_GEMM_TAIL") ? std::atoi(std::getenv("LCN_GEMM_TAIL")) : 16;
+  return t;
+}
 
 int gemm(Handle* h, const GemmCall& c, int B) {
   if (c.X.mode == PRO_BNBACK) {
@@ -645,6 +663,8 @@ int gemm(Handle* h, const GemmCall& c, int B) {
   a.blocks = c.blocks;
   a.ptr = c.ptr;
   a.idx = c.idx;
+  a.order = c.order;
+  a.tail = tail_groups();
   a.bias = c.bias;
   a.pro_mode = c.X.mode;
   if (c.X.mode == PRO_BNACT) {
@@ -687,7 +707,8 @@ int gemm_hidden(Handle* h, int k, int kindt, const Operand& X, float* Y, const f
   GemmCall c{X, fwd ? Lr.blk_fwd : Lr.blk_bwd, fwd ? h->fwd_ptr : h->bwd_ptr,
              fwd ? h->fwd_idx : h->bwd_idx, h->nslab, fwd ? h->theta + h->b_off[k] : nullptr,
              Y, h->nslab, addsrc, epi_mode, epi_layer,
-             kindt, 2.0 * 4096.0 * h->nblk};  // 2*64*64 FLOP per block per row
+             kindt, 2.0 * 4096.0 * h->nblk,   // 2*64*64 FLOP per block per row
+             fwd ? h->fwd_order : h->bwd_order};
   return gemm(h, c, B);
 }
 

@@ -109,6 +109,8 @@ struct GemmArgs {
   const float* blocks;               // fragment-packed blocks
   const int* ptr;                    // [n_out_slabs + 1]
   const int2* idx;                   // (in_slab, block id)
+  const int* order;                  // output slabs by falling list length (tail schedule), or null
+  int tail;                          // row-tile groups per XCD scheduled longest-list-first at the end
   const float* bias;                 // [n_out_slabs*64] or null
   int pro_mode;                      // PRO_RAW or PRO_BNACT
   const float* pro_scale;            // forward BN scale / shift of the input's layer [F]
