@@ -341,6 +341,9 @@ def main(argv=None):
             kern[name] = {"launches": n, "avg_ms": ms / n, "tflops": fl / (ms * 1e-3) / 1e12,
                           "total_ms_per_step": ms / args.steps}
     bn_act_timing = net.kernel_timing(native.K_BN_ACT)
+    thin_timing = {name: net.kernel_timing(kid) for name, kid in (
+        ("lift (x . W1e + b1, BN statistics)", native.K_LIFT),
+        ("output (h . W4e)", native.K_OUT), ("output weight gradient (h^T dy)", native.K_OUT_DW))}
     net.set_timing(False)
 
     # forward-only rate (BASELINE configs[1], cfg2) on the same resident batch
@@ -397,6 +400,15 @@ def main(argv=None):
                       "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                       "frac_of_achievable": round(gbs / HBM_ACHIEVABLE_GBS, 4),
                       "achievable": HBM_ACHIEVABLE_GBS}
+        # the thin lift / output layers are HBM-bound too: algorithmic bytes =
+        # input rows read + output rows written
+        hbm_thin = []
+        for name, (nt, mst, bt) in thin_timing.items():
+            if nt:
+                gbs = bt / (mst * 1e-3) / 1e9
+                hbm_thin.append({"kernel": name, "launches": nt, "avg_ms": round(mst / nt, 4),
+                                 "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(gbs / HBM_PEAK_GBS, 4)})
         hbm = None
         if "gemm_fwd" in kern:
             f = kern["gemm_fwd"]
@@ -428,6 +440,7 @@ def main(argv=None):
             "roofline": roof,
             "hbm": hbm,
             "hbm_elementwise": hbm_ew,
+            "hbm_thin_layers": hbm_thin,
             "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv for kk, vv in v.items()}
                         for k, v in kern.items()},
             "fwd_only_poses_per_s": round(G * nf / tfwd, 1),

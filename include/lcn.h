@@ -240,8 +240,12 @@ uint32_t lcn_crc32c(uint32_t crc, const void* data, int64_t n);
 /* --- instrumentation --------------------------------------------------- */
 /* kernel ids for lcn_kernel_timing */
 /* LCN_K_BN_ACT: the BN apply + LeakyReLU (+ residual) pass that materialises
- * the block outputs; its "flops" field accumulates algorithmic HBM bytes */
-enum { LCN_K_GEMM_FWD = 0, LCN_K_GEMM_DX = 1, LCN_K_GEMM_DW = 2, LCN_K_BN_ACT = 3, LCN_K_NUM = 4 };
+ * the block outputs; LCN_K_LIFT / LCN_K_OUT / LCN_K_OUT_DW: the thin lift
+ * (models_att.py:729) and output (:765) layers' forward launches and the
+ * output layer's weight gradient.  For these HBM-bound kernels the "flops"
+ * field accumulates algorithmic HBM bytes (inputs read + outputs written). */
+enum { LCN_K_GEMM_FWD = 0, LCN_K_GEMM_DX = 1, LCN_K_GEMM_DW = 2, LCN_K_BN_ACT = 3, LCN_K_LIFT = 4,
+       LCN_K_OUT = 5, LCN_K_OUT_DW = 6, LCN_K_NUM = 7 };
 int lcn_set_timing(void* handle, int32_t enable);
 int lcn_kernel_timing(void* handle, int32_t kernel, int64_t* launches, double* total_ms,
                       double* flops);

@@ -72,12 +72,18 @@ namespace lcn {
     float4* d_ = Wl + (BUF) * 1024 + (threadIdx.x & ~63);                 \
     GLDS(ws_, d_) GLDS(ws_ + 256, d_ + 256) GLDS(ws_ + 512, d_ + 512) GLDS(ws_ + 768, d_ + 768) \
   }
+// BN apply + LeakyReLU of one activation fragment (k-group G of a slab whose
+// first channel is CH), scale / shift from the LDS tables
+#define TSTEP(G, XV, CH)                                                  \
+  {                                                                       \
+    const int c_ = (CH) + 8 * (G) + 4 * h;                                \
+    XV = bnact4(XV, *(const float4*)(tsc + c_), *(const float4*)(tsh + c_), al); \
+  }
+#define TRANSX(P, CH)                                                     \
+  TSTEP(0, P##0, CH) TSTEP(1, P##1, CH) TSTEP(2, P##2, CH) TSTEP(3, P##3, CH) \
+  TSTEP(4, P##4, CH) TSTEP(5, P##5, CH) TSTEP(6, P##6, CH) TSTEP(7, P##7, CH)
 #define GSTEP(BUF, G, XV, CH)                                             \
   {                                                                       \
-    if constexpr (PRO == PRO_BNACT) {                                     \
-      const int c_ = (CH) + 8 * (G) + 4 * h;                              \
-      XV = bnact4(XV, *(const float4*)(tsc + c_), *(const float4*)(tsh + c_), al); \
-    }                                                                     \
     const float4 w0_ = Wl[(BUF) * 1024 + (2 * (G)) * 64 + lane];          \
     const float4 w1_ = Wl[(BUF) * 1024 + (2 * (G) + 1) * 64 + lane];      \
     STEP(w0_, w1_, XV)                                                    \
@@ -91,7 +97,13 @@ namespace lcn {
   SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) SGB(0x008, 8)               \
   SGB(0x100, DSR) SGB(0x008, 8) SGB(0x100, DSR) SGB(0x008, 8)               \
   SGB(0x100, DSR) SGB(0x008, 8) SGB(0x008, 8)
+// PRO_BNACT: the slab's eight fragments are transformed in one block ahead of
+// its MFMAs (16 table reads in flight together, then 96 VALU operations the
+// other waves of the SIMD cover); done per k-group between the MFMAs, every
+// group waited for its own table reads (842 vs 805 us, gemm_bench cfg3)
+#define COMPX_PRE(P, CH) if constexpr (PRO == PRO_BNACT) { TRANSX(P, CH) __builtin_amdgcn_sched_barrier(0); }
 #define COMPX(BUF, P, CH)                                                 \
+  COMPX_PRE(P, CH)                                                        \
   GSTEP(BUF, 0, P##0, CH) GSTEP(BUF, 1, P##1, CH) GSTEP(BUF, 2, P##2, CH) \
   GSTEP(BUF, 3, P##3, CH) GSTEP(BUF, 4, P##4, CH) GSTEP(BUF, 5, P##5, CH) \
   GSTEP(BUF, 6, P##6, CH) GSTEP(BUF, 7, P##7, CH) SCHED_SLAB
@@ -145,7 +157,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   const float* tsc = nullptr;
   const float* tsh = nullptr;
   const int spj = a.spj_in;
-  constexpr int DSR = PRO == PRO_BNACT ? 4 : 2;  // LDS reads per k-group
+  constexpr int DSR = 2;  // weight reads per k-group
 
   // the first weight block and activation fragments go in flight first; the
   // bias / residual / table loads below are batched behind them, so the

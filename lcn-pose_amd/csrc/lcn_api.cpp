@@ -717,8 +717,9 @@ int gemm_hidden(Handle* h, int k, int kindt, const Operand& X, float* Y, const f
 // stored to dz_out when given): partial slabs per batch chunk, then a
 // fixed-order reduce into the raw-gradient vector (rows / columns past the
 // valid range are padding and are dropped)
+// `timer`: LCN_K_GEMM_DW (FLOPs), LCN_K_OUT_DW (algorithmic bytes) or -1 (not timed)
 int gemm_dw(Handle* h, const Operand& A, const Operand& D, const int2* blk, int nblk, float* dW,
-            int ld, int rows_valid, int cols_valid, int B, bool timed, float* dz_out = nullptr) {
+            int ld, int rows_valid, int cols_valid, int B, int timer, float* dz_out = nullptr) {
   GemmDwArgs a{};
   a.A = A.p;
   a.S_a = A.S;
@@ -753,9 +754,10 @@ int gemm_dw(Handle* h, const Operand& A, const Operand& D, const int2* blk, int 
   a.nchunks = (int)cdiv(B, a.chunk_rows);
   a.part = h->dw_part;
   hipEvent_t ev[2];
-  if (timed) tstart(h, LCN_K_GEMM_DW, ev);
+  if (timer >= 0) tstart(h, timer, ev);
   launch_gemm_dw(a, h->stream);
-  if (timed) tstop(h, LCN_K_GEMM_DW, ev, 2.0 * 4096.0 * nblk * B);
+  if (timer >= 0)
+    tstop(h, timer, ev, timer == LCN_K_GEMM_DW ? 2.0 * 4096.0 * nblk * B : 4.0 * (h->H + 51) * (double)B);
   launch_dw_reduce(h->dw_part, a.nchunks, nblk, blk, dW, ld, rows_valid, cols_valid, h->stream);
   return LCN_OK;
 }
@@ -807,9 +809,11 @@ int forward(Handle* h, int B, bool with_labels, bool train) {
   CHECK(prep_weights(h));
   const int epi = h->batch_norm ? EPI_BNFWD : EPI_NONE;
   // lift z0 = x . W1e + b1 (models_att.py:714-729): x padded to one 64-wide slab
-  const double thin_flops = 2.0 * 4096.0 * h->nslab;
+  // the thin layers are HBM-bound: their timers accumulate algorithmic bytes
+  // per row (input read + output written)
+  const double lift_bytes = 4.0 * (kJ * h->inF + h->H), out_bytes = 4.0 * (h->H + 51);
   CHECK(gemm(h, GemmCall{raw(h->x, 1), h->wl[0].blk_fwd, h->thin_ptr, h->thin_idx, S,
-                         h->theta + h->b_off[0], h->Z[0], S, nullptr, epi, -1, -1, thin_flops}, B));
+                         h->theta + h->b_off[0], h->Z[0], S, nullptr, epi, -1, LCN_K_LIFT, lift_bytes}, B));
   CHECK(bn_stats(h, 0, B));
   bn_act_timed(h, h->Z[0], nullptr, h->Hb[0], 0, B);
   // two_linear blocks (models_att.py:630-705)
@@ -832,7 +836,7 @@ int forward(Handle* h, int B, bool with_labels, bool train) {
   // output layer y = h_L . W4e + b4 into a 1-slab buffer (51 used), then the
   // output assembly, loss and d out (models_att.py:749-773, :356)
   CHECK(gemm(h, GemmCall{raw(h->Hb[h->L], S), h->wl[nl - 1].blk_fwd, h->out_ptr, h->out_idx, 1,
-                         nullptr, h->yout, 1, nullptr, EPI_NONE, -1, -1, thin_flops}, B));
+                         nullptr, h->yout, 1, nullptr, EPI_NONE, -1, LCN_K_OUT, out_bytes}, B));
   OutAsmArgs oa{};
   oa.y = h->yout;
   oa.b4 = h->theta + h->b_off[nl - 1];
@@ -865,7 +869,7 @@ int backward(Handle* h, int B) {
   CHECK(gemm(h, GemmCall{raw(h->dy, 1), Lo.blk_bwd, h->thin_ptr, h->thin_idx, S, nullptr,
                          h->DH, S, nullptr, EPI_BNBACK, top, -1, 0.0}, B));
   CHECK(gemm_dw(h, raw(h->Hb[L], S), raw(h->dy, 1), h->out_blk, S, h->rg + Lo.w_off, 51,
-                H, 51, B, false));
+                H, 51, B, LCN_K_OUT_DW));
   const int ct = (int)cdiv(B, kEwRows);
   launch_colpart(h->dy, B, 51, h->col_part, s);
   launch_colreduce(h->col_part, ct, kEwRows, B, 51, 0, h->colacc, s);
@@ -878,12 +882,12 @@ int backward(Handle* h, int B) {
     CHECK(bn_back(h, k2, B));
     const Operand g = h->drop_on ? raw(h->Gb[l], S) : Operand{h->Z[k1], S, PRO_BNACT, k1};
     CHECK(gemm_dw(h, g, Operand{h->DH, S, PRO_BNBACK, k2},
-                  h->blk, h->nblk, h->rg + h->wl[k2].w_off, H, H, H, B, true,
+                  h->blk, h->nblk, h->rg + h->wl[k2].w_off, H, H, H, B, LCN_K_GEMM_DW,
                   h->DZ));                                             // dW_k2 = g^T dz2; DZ = dz2
     CHECK(gemm_hidden(h, k2, LCN_K_GEMM_DX, raw(h->DZ, S), h->DG, nullptr, EPI_BNBACK, k1, B));
     CHECK(bn_back(h, k1, B));
     CHECK(gemm_dw(h, raw(h->Hb[l], S), Operand{h->DG, S, PRO_BNBACK, k1}, h->blk, h->nblk,
-                  h->rg + h->wl[k1].w_off, H, H, H, B, true,
+                  h->rg + h->wl[k1].w_off, H, H, H, B, LCN_K_GEMM_DW,
                   h->DZ));                                             // dW_k1 = h_l^T dz1; DZ = dz1
     CHECK(gemm_hidden(h, k1, LCN_K_GEMM_DX, raw(h->DZ, S), h->DH, h->residual ? h->DH : nullptr,
                       EPI_BNBACK, below, B));                          // dh_l (+ residual)
@@ -891,7 +895,7 @@ int backward(Handle* h, int B) {
   // lift: dz0, dW1e = x^T dz0 (x padded: rows >= 17*in_F dropped), db1
   CHECK(bn_back(h, 0, B));
   CHECK(gemm_dw(h, raw(h->x, 1), Operand{h->DH, S, PRO_BNBACK, 0}, h->lift_blk, S,
-                h->rg + h->wl[0].w_off, H, kJ * h->inF, H, B, false));
+                h->rg + h->wl[0].w_off, H, kJ * h->inF, H, B, -1));
   return LCN_OK;
 }
 

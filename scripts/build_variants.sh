@@ -6,7 +6,7 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 cd $R/lcn-pose_amd/csrc
 for v in ${VARIANTS:-base:}; do
-  n=${v%%:*}; f=${v#*:}
+  n=${v%%:*}; f=${v#*:}; f=${f//+/ }
   make gemm_bench BUILD=build_$n EXTRA="$f" -j8 2>&1 | grep -E "error|Error" || true
   test -x build_$n/gemm_bench
 done

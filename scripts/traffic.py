@@ -45,8 +45,11 @@ def main(out_dir):
             sel = [(g, v) for (_, n, g, v) in rows if classify(n) == cls]
             if not sel:
                 continue
+            # the thin lift / output launches share kernel and grid with the
+            # hidden layers but move a fraction of the bytes: keep the big launches
             gmax = max(g for g, _ in sel)
-            vals = [v * scale for g, v in sel if g == gmax]
+            vmax = max(v for g, v in sel if g == gmax)
+            vals = [v * scale for g, v in sel if g == gmax and v > 0.5 * vmax]
             per[tag] = sum(vals) / len(vals)
             per["launches_" + tag] = len(vals)
         if "read" in per and "write" in per:
