@@ -77,16 +77,53 @@ __device__ __forceinline__ void colsum_groups_lds(const double2* __restrict__ co
   __syncthreads();
 }
 
+// The same column sums straight from the GEMM's tile partials part[n_tiles][H]
+// (float64, tiles in order; mode as colreduce), for launches of few tiles:
+// one kernel instead of colreduce + finish.
+__device__ __forceinline__ void colsum_tiles_lds(const float2* __restrict__ part, int n_tiles,
+                                                 int tile_rows, int B, int H, int mode, double2* cs) {
+  for (int c = threadIdx.x; c < H; c += blockDim.x) {
+    double x = 0.0, y = 0.0;
+    float2 pv[8];  // n_tiles <= 8: all loads in flight together
+#pragma unroll
+    for (int t = 0; t < 8; ++t) pv[t] = t < n_tiles ? part[(size_t)t * H + c] : make_float2(0.f, 0.f);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      if (t >= n_tiles) break;
+      const float2 v = pv[t];
+      x += (double)v.x;
+      if (mode == 1) {
+        const double nt = (double)min(tile_rows, B - t * tile_rows);
+        y += (double)v.y + (double)v.x * (double)v.x / nt;
+      } else {
+        y += (double)v.y;
+      }
+    }
+    cs[c] = make_double2(x, y);
+  }
+  __syncthreads();
+}
+
+// Where the finish kernels take their column sums from: colreduce's tile-group
+// sums (part == null) or the tile partials themselves.
+struct ColSrc {
+  const double2* col;
+  const float2* part; int n_tiles, tile_rows, B;
+};
+
 // Forward BN finish per channel.  Phase 0: complete; 1: local channel sums ->
 // acc[2F] (and stop); 2: finish from the all-reduced acc.  zsum (when given)
 // receives the per-column sums of z (bias-gradient term of the backward).
 __global__ __launch_bounds__(1024) void bn_fwd_finalize_kernel(
-    const double2* __restrict__ col, int H, int F, int phase, double rows,
+    ColSrc src, int H, int F, int phase, double rows,
     const RowInfo* __restrict__ ri, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, double* acc, BnStats st,
     double* __restrict__ zsum) {
   extern __shared__ double2 cs[];  // [H]
-  if (phase <= 1) colsum_groups_lds(col, H, cs);
+  if (phase <= 1) {
+    if (src.part) colsum_tiles_lds(src.part, src.n_tiles, src.tile_rows, src.B, H, 1, cs);
+    else colsum_groups_lds(src.col, H, cs);
+  }
   const int J = H / F;
   const double count = (ri ? ri->rows_global : rows) * (double)J;
   for (int ch = threadIdx.x; ch < F; ch += blockDim.x) {
@@ -115,10 +152,11 @@ __global__ __launch_bounds__(1024) void bn_fwd_finalize_kernel(
   }
 }
 
-void launch_bn_fwd_finalize(const double2* col, int H, int F, int phase, double rows,
-                            const RowInfo* ri, const float* gamma, const float* beta, float eps,
-                            double* acc, BnStats st, double* zsum, hipStream_t s) {
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(1), dim3(1024), H * sizeof(double2), s, col, H,
+void launch_bn_fwd_finalize(const double2* col, const TilePartials& tp, int H, int F, int phase,
+                            double rows, const RowInfo* ri, const float* gamma, const float* beta,
+                            float eps, double* acc, BnStats st, double* zsum, hipStream_t s) {
+  const ColSrc src{col, tp.part, tp.n_tiles, tp.tile_rows, tp.B};
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(1), dim3(1024), H * sizeof(double2), s, src, H,
                      F, phase, rows, ri, gamma, beta, eps, acc, st, zsum);
 }
 
@@ -131,13 +169,14 @@ void launch_bn_fwd_finalize(const double2* col, int H, int F, int phase, double 
 // all-reduced later); c123 uses the global sums.  bn = 0 (no BatchNorm):
 // dz = du and only db is written.  Phases as bn_fwd_finalize.
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
-    const double2* __restrict__ col, int H, int F, int phase, int bn, double rows,
+    ColSrc src, int H, int F, int phase, int bn, double rows,
     const RowInfo* __restrict__ ri, double b_local, const float* __restrict__ gamma,
     const float* __restrict__ mean, const float* __restrict__ rstd, double* acc,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ c123,
     const double* __restrict__ zsum, float* __restrict__ db) {
   extern __shared__ double2 cs[];  // [H]
-  colsum_groups_lds(col, H, cs);
+  if (src.part) colsum_tiles_lds(src.part, src.n_tiles, src.tile_rows, src.B, H, 0, cs);
+  else colsum_groups_lds(src.col, H, cs);
   const int J = H / F;
   const double count = (ri ? ri->rows_global : rows) * (double)J;
   for (int ch = threadIdx.x; ch < F; ch += blockDim.x) {
@@ -173,12 +212,13 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
   }
 }
 
-void launch_bn_bwd_finalize(const double2* col, int H, int F, int phase, int bn, double rows,
-                            const RowInfo* ri, double b_local, const float* gamma,
-                            const float* mean, const float* rstd, double* acc, float* dgamma,
-                            float* dbeta, float* c123, const double* zsum, float* db,
+void launch_bn_bwd_finalize(const double2* col, const TilePartials& tp, int H, int F, int phase,
+                            int bn, double rows, const RowInfo* ri, double b_local,
+                            const float* gamma, const float* mean, const float* rstd, double* acc,
+                            float* dgamma, float* dbeta, float* c123, const double* zsum, float* db,
                             hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(1024), H * sizeof(double2), s, col, H,
+  const ColSrc src{col, tp.part, tp.n_tiles, tp.tile_rows, tp.B};
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(1024), H * sizeof(double2), s, src, H,
                      F, phase, bn, rows, ri, b_local, gamma, mean, rstd, acc, dgamma, dbeta, c123,
                      zsum, db);
 }

@@ -43,11 +43,20 @@ __global__ __launch_bounds__(256) void wnorm_part_kernel(const float* __restrict
   const int l = blockIdx.y, p = blockIdx.x;
   const float* w = params + offs[l];
   const int64_t n = sizes[l];
-  double s = 0.0;
-  for (int64_t i = (int64_t)p * 256 + threadIdx.x; i < n; i += (int64_t)ppl * 256) {
-    const double v = w[i];
-    s += v * v;
+  // four independent chains per thread: the float64 multiply-adds are
+  // latency bound otherwise (fixed order, deterministic)
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  const int64_t stride = (int64_t)ppl * 256;
+  int64_t i = (int64_t)p * 256 + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const double v0 = w[i], v1 = w[i + stride], v2 = w[i + 2 * stride], v3 = w[i + 3 * stride];
+    s0 += v0 * v0; s1 += v1 * v1; s2 += v2 * v2; s3 += v3 * v3;
   }
+  for (; i < n; i += stride) {
+    const double v = w[i];
+    s0 += v * v;
+  }
+  double s = (s0 + s1) + (s2 + s3);
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
@@ -80,16 +89,20 @@ void launch_wnorm(const float* params, const int64_t* offs, const int64_t* sizes
 
 // hidden layer: one workgroup per 64x64 block (si, so) of W_e:
 // fwd block [n = q][k = p] (z = a.We), bwd block [n = p][k = q] (da = dz.We^T)
-__global__ __launch_bounds__(256) void wprep_hidden_kernel(const float* __restrict__ W, int ld,
-                                                           const int2* __restrict__ blk, int spj,
-                                                           const float* __restrict__ M,
-                                                           const float* __restrict__ denom, int layer,
-                                                           float* __restrict__ fwd,
-                                                           float* __restrict__ bwd) {
+// (all hidden layers in one launch: blockIdx.y picks the layer)
+__global__ __launch_bounds__(256) void wprep_hidden_kernel(const float* __restrict__ params,
+                                                           const WPrepHidden* __restrict__ items,
+                                                           int ld, const int2* __restrict__ blk,
+                                                           int spj, const float* __restrict__ M,
+                                                           const float* __restrict__ denom) {
   const int b = blockIdx.x;
+  const WPrepHidden it = items[blockIdx.y];
+  const float* __restrict__ W = params + it.w_off;
+  float* __restrict__ fwd = it.fwd;
+  float* __restrict__ bwd = it.bwd;
   const int2 sb = blk[b];
   const float m = M[(sb.x / spj) * kJ + (sb.y / spj)];
-  const float dn = denom[layer];
+  const float dn = denom[it.layer];
   for (int e = threadIdx.x; e < 4096; e += 256) {
     const int p = e >> 6, q = e & 63;
     const float v = (W[(size_t)(sb.x * 64 + p) * ld + sb.y * 64 + q] / dn) * m;
@@ -134,14 +147,18 @@ __global__ __launch_bounds__(256) void wprep_out_kernel(const float* __restrict_
   }
 }
 
+void launch_wprep_hidden(const float* params, const WPrepHidden* items, int n_layers, int ld,
+                         const int2* blk, int nblk, int spj, const float* M, const float* denom,
+                         hipStream_t s) {
+  if (n_layers <= 0) return;
+  hipLaunchKernelGGL(wprep_hidden_kernel, dim3(nblk, n_layers), dim3(256), 0, s, params, items, ld, blk,
+                     spj, M, denom);
+}
+
 void launch_wprep(const float* params, const WLayer& L, const float* M, const float* denom,
                   int layer, hipStream_t s) {
   const float* W = params + L.w_off;
-  if (L.kind == 1) {
-    const int spj = L.fin / 64;
-    hipLaunchKernelGGL(wprep_hidden_kernel, dim3(L.nblk), dim3(256), 0, s, W, L.nout, L.blk, spj, M,
-                       denom, layer, L.blk_fwd, L.blk_bwd);
-  } else if (L.kind == 0) {
+  if (L.kind == 0) {
     const int nslab = L.nout / 64, spj = L.fout / 64;
     hipLaunchKernelGGL(wprep_lift_kernel, dim3(nslab), dim3(256), 0, s, W, L.fin, nslab, spj, M,
                        denom, layer, L.blk_fwd);

@@ -78,9 +78,10 @@ struct Handle {
   // mask / norms
   float *Md = nullptr, *Sd = nullptr, *Cd = nullptr, *denom = nullptr, *lcoef = nullptr;
   double *norm_part = nullptr, *norm2 = nullptr, *blocksum = nullptr;
+  WPrepHidden* wprep_items = nullptr;   // the hidden layers, for the one-launch weight prep
   int64_t *w_offs = nullptr, *w_sizes = nullptr;
   int *w_kin = nullptr, *w_nout = nullptr;
-  int norm_ppl = 64;
+  int norm_ppl = 256;
 
   // activations
   // x / y / dy of the thin layers are padded to 64 columns (pads stay zero)
@@ -107,7 +108,8 @@ struct Handle {
   std::vector<double*> zsum;      // per BN layer: column sums of z (bias-gradient term)
   float *ident_scale = nullptr, *ident_shift = nullptr, *ident_c123 = nullptr;
   float* c123 = nullptr;
-  float2* stat_part = nullptr;    // [B/128 tiles][H] GEMM epilogue partials
+  float2* stat_part = nullptr;    // GEMM epilogue partials [tiles][H], tiles of stat_rows rows
+  int stat_rows = kGemmRows;      // rows per partial of the last GEMM: 128, or 32 (small-batch kernel)
   float2* col_part = nullptr;     // [B/kEwRows tiles][51] output-bias partials
   double2* colacc = nullptr;      // [kColSplit][H] float64 column sums
   float* dw_part = nullptr;
@@ -240,6 +242,15 @@ int dw_chunks(int nblk) {
   static const int budget = std::getenv("LCN_DW_ROWS") ? std::atoi(std::getenv("LCN_DW_ROWS")) : 5600;
   static const int cap = std::getenv("LCN_DW_MAXCH") ? std::atoi(std::getenv("LCN_DW_MAXCH")) : 64;
   return std::max(1, std::min(cap, budget / std::max(1, nblk)));
+}
+
+// Launches of at most this many 32-row tiles run the small-batch kernel, which
+// splits every slab list over the four waves of a workgroup: measured faster
+// up to batch 1024 (0.92 -> 0.63 ms per step at batch 200, 1.24 -> 1.09 ms at
+// 1024), slower from 2048 on.  LCN_SMALL_RT overrides, 0 = never.
+int small_row_tiles() {
+  static const int t = std::getenv("LCN_SMALL_RT") ? std::atoi(std::getenv("LCN_SMALL_RT")) : 40;
+  return t;
 }
 
 // ---------------------------------------------------------------------------
@@ -396,6 +407,12 @@ int build(Handle* h, const lcn_config* c) {
       CHECK(dalloc(h, &Lr.blk_bwd, (size_t)h->nslab * 4096));
     }
   }
+  {
+    std::vector<WPrepHidden> items;
+    for (int k = 0; k < nl; ++k)
+      if (h->wl[k].kind == 1) items.push_back(WPrepHidden{h->wl[k].w_off, h->wl[k].blk_fwd, h->wl[k].blk_bwd, k});
+    CHECK(upload(h, &h->wprep_items, items));
+  }
   // norms: entries [0, nl) are the weights (clip_by_norm), [nl, 2nl) the biases
   // (only for the l2 regularisation term of the reported loss)
   std::vector<int64_t> wo(2 * nl), ws(2 * nl);
@@ -495,7 +512,8 @@ int build(Handle* h, const lcn_config* c) {
     }
   }
   CHECK(dalloc(h, &h->c123, 3 * F));
-  CHECK(dalloc(h, &h->stat_part, (size_t)cdiv(B, kGemmRows) * H));
+  CHECK(dalloc(h, &h->stat_part,
+               (size_t)std::max<int64_t>(cdiv(B, kGemmRows), std::min<int64_t>(cdiv(B, kRT), small_row_tiles())) * H));
   CHECK(dalloc(h, &h->col_part, (size_t)cdiv(B, kEwRows) * 64));
   CHECK(dalloc(h, &h->colacc, (size_t)kColSplit * H));
   h->loss_grid = (int)std::min<int64_t>(2048, cdiv(B, 4));
@@ -594,8 +612,21 @@ int prep_weights(Handle* h) {
   launch_mask(h->learnable ? h->theta + h->mask_off : nullptr, h->Cd, h->learnable, h->Md, h->Sd, s);
   launch_wnorm(h->theta, h->w_offs, h->w_sizes, 2 * h->nl, h->norm_part, h->norm_ppl, h->norm2,
                h->denom, h->max_norm, s);
-  for (int k = 0; k < h->nl; ++k) launch_wprep(h->theta, h->wl[k], h->Md, h->denom, k, s);
+  launch_wprep_hidden(h->theta, h->wprep_items, 2 * h->L, h->H, h->blk, h->nblk, h->spj, h->Md, h->denom, s);
+  launch_wprep(h->theta, h->wl[0], h->Md, h->denom, 0, s);
+  launch_wprep(h->theta, h->wl[h->nl - 1], h->Md, h->denom, h->nl - 1, s);
   return LCN_OK;
+}
+
+// The last GEMM's epilogue partials for the BN finish kernels: with at most 8
+// tiles (batch <= 256 behind the small-batch GEMM, <= 1024 otherwise) the
+// finish sums them itself -- a colreduce launch costs ~4 us, as much as the
+// whole reduction then; with more tiles the one finishing workgroup's serial
+// walk over them is slower than the extra launch (measured at 32 and 64 tiles)
+TilePartials tile_partials(const Handle* h, int B) {
+  const int n_tiles = (int)cdiv(B, h->stat_rows);
+  if (n_tiles > 8) return TilePartials{nullptr, 0, 0, 0};
+  return TilePartials{h->stat_part, n_tiles, h->stat_rows, B};
 }
 
 // BN statistics of BN layer k from the EPI_BNFWD partials its GEMM wrote
@@ -608,16 +639,17 @@ int bn_stats(Handle* h, int k, int B) {
   const RowInfo* ri = rinfo(h);
   const float* gamma = h->theta + h->gamma_off[k];
   const float* beta = h->theta + h->beta_off[k];
-  launch_colreduce(h->stat_part, (int)cdiv(B, kGemmRows), kGemmRows, B, h->H, 1, h->colacc, s);
+  const TilePartials tp = tile_partials(h, B);
+  if (!tp.part) launch_colreduce(h->stat_part, (int)cdiv(B, h->stat_rows), h->stat_rows, B, h->H, 1, h->colacc, s);
   if (!h->phased && !multi(h)) {
-    launch_bn_fwd_finalize(h->colacc, h->H, h->F, 0, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
+    launch_bn_fwd_finalize(h->colacc, tp, h->H, h->F, 0, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
                            h->zsum[k], s);
     return LCN_OK;
   }
-  launch_bn_fwd_finalize(h->colacc, h->H, h->F, 1, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
+  launch_bn_fwd_finalize(h->colacc, tp, h->H, h->F, 1, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
                          h->zsum[k], s);
   CHECK(allreduce(h, h->acc1, 2 * h->F, ncclDouble));
-  launch_bn_fwd_finalize(h->colacc, h->H, h->F, 2, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
+  launch_bn_fwd_finalize(h->colacc, tp, h->H, h->F, 2, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
                          nullptr, s);
   return LCN_OK;
 }
@@ -692,9 +724,14 @@ int gemm(Handle* h, const GemmCall& c, int B) {
   a.B = B;
   a.n_out_slabs = c.n_out_slabs;
   a.n_rt = (int)cdiv(B, kRT);
+  // few row tiles: the kernel that splits the slab lists over a workgroup's
+  // waves (no dropout epilogue there); its BN partials are per 32-row tile
+  const bool small = a.n_rt <= small_row_tiles() && !(c.epi_mode == EPI_BNBACK && a.epi_drop.rate > 0.f);
+  h->stat_rows = small ? kRT : kGemmRows;
   hipEvent_t ev[2];
   if (c.timer >= 0) tstart(h, c.timer, ev);
-  launch_gemm_bs(a, h->stream);
+  if (small) launch_gemm_bs_small(a, h->stream);
+  else launch_gemm_bs(a, h->stream);
   if (c.timer >= 0) tstop(h, c.timer, ev, c.flops_per_row * B);
   return LCN_OK;
 }
@@ -776,16 +813,17 @@ int bn_back(Handle* h, int k, int B) {
   float* dgam = bn ? h->rg + h->gamma_off[k] : nullptr;
   float* dbet = bn ? h->rg + h->beta_off[k] : nullptr;
   float* db = h->rg + h->b_off[k];
-  launch_colreduce(h->stat_part, (int)cdiv(B, kGemmRows), kGemmRows, B, h->H, 0, h->colacc, s);
+  const TilePartials tp = tile_partials(h, B);
+  if (!tp.part) launch_colreduce(h->stat_part, (int)cdiv(B, h->stat_rows), h->stat_rows, B, h->H, 0, h->colacc, s);
   if ((!h->phased && !multi(h)) || !bn) {
-    launch_bn_bwd_finalize(h->colacc, h->H, h->F, 0, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
+    launch_bn_bwd_finalize(h->colacc, tp, h->H, h->F, 0, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
                            h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
     return LCN_OK;
   }
-  launch_bn_bwd_finalize(h->colacc, h->H, h->F, 1, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
+  launch_bn_bwd_finalize(h->colacc, tp, h->H, h->F, 1, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
                          h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
   CHECK(allreduce(h, h->acc1, 2 * h->F, ncclDouble));
-  launch_bn_bwd_finalize(h->colacc, h->H, h->F, 2, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
+  launch_bn_bwd_finalize(h->colacc, tp, h->H, h->F, 2, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
                          h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
   return LCN_OK;
 }

@@ -129,6 +129,10 @@ struct GemmArgs {
   int B; int n_out_slabs; int n_rt;  // n_rt = ceil(B / 32)
 };
 void launch_gemm_bs(const GemmArgs& a, hipStream_t s);
+// the same for launches of few row tiles (gemm_small.hip): one row tile per
+// workgroup, the slab list split over its waves; stat gets one partial per
+// 32-row tile (not per 128-row group); no dropout epilogue
+void launch_gemm_bs_small(const GemmArgs& a, hipStream_t s);
 
 // dWe blocks: part[chunk][blk][p][q] = sum_{b in chunk} A[b, si*64+p] * D[b, so*64+q]
 // Work unit = a group of up to 2 blocks with the same output slab so (they
@@ -229,18 +233,23 @@ struct BnStats { float* mean; float* rstd; float* scale; float* shift; };
 constexpr int kColSplit = 8;
 void launch_colreduce(const float2* part, int n_tiles, int tile_rows, int B, int H, int mode,
                       double2* out, hipStream_t s);
+// The GEMM epilogue's tile partials, handed to the finish kernels directly when
+// a launch has few tiles (part == null: they read colreduce's sums instead).
+struct TilePartials {
+  const float2* part; int n_tiles, tile_rows, B;
+};
 // forward BN finish from colreduce mode-1 sums.  phase 0 complete (single GPU);
 // 1 local channel sums -> acc[2F]; 2 finish from all-reduced acc.  The element
 // count per channel is rows_global * J, rows_global = `rows` or, when ri is
 // given, ri->rows_global.  zsum (optional): per-column sum of z.
-void launch_bn_fwd_finalize(const double2* col, int H, int F, int phase, double rows,
-                            const RowInfo* ri,
+void launch_bn_fwd_finalize(const double2* col, const TilePartials& tp, int H, int F, int phase,
+                            double rows, const RowInfo* ri,
                             const float* gamma, const float* beta, float eps, double* acc,
                             BnStats st, double* zsum, hipStream_t s);
 // backward BN finish from colreduce mode-0 sums of (du, du*zhat): c1|c2|c3,
 // local dgamma/dbeta and the bias gradient db; bn = 0: db = sum du only
-void launch_bn_bwd_finalize(const double2* col, int H, int F, int phase, int bn, double rows,
-                            const RowInfo* ri, double b_local, const float* gamma, const float* mean,
+void launch_bn_bwd_finalize(const double2* col, const TilePartials& tp, int H, int F, int phase,
+                            int bn, double rows, const RowInfo* ri, double b_local, const float* gamma, const float* mean,
                             const float* rstd, double* acc, float* dgamma, float* dbeta,
                             float* c123, const double* zsum, float* db, hipStream_t s);
 // h = [res +] leaky(scale*z + shift), tiled [B][S*64] buffers
@@ -277,9 +286,18 @@ void launch_mask(const float* V, const float* Cmat, int learnable, float* M, flo
 void launch_wnorm(const float* params, const int64_t* offs, const int64_t* sizes, int nl,
                   double* part, int parts_per_layer, double* norm2, float* denom, int max_norm,
                   hipStream_t s);
-// W_e = (W / denom) * M[i,j]; writes the layer's packed / dense / coef forms
+// W_e = (W / denom) * M[i,j]; writes the layer's packed forms (thin layers)
 void launch_wprep(const float* params, const WLayer& L, const float* M, const float* denom,
                   int layer, hipStream_t s);
+// the same for all hidden layers in one launch
+struct WPrepHidden {
+  int64_t w_off;           // the layer's weight in the flat parameter vector
+  float* fwd; float* bwd;  // its packed block arrays
+  int layer;               // index into denom
+};
+void launch_wprep_hidden(const float* params, const WPrepHidden* items, int n_layers, int ld,
+                         const int2* blk, int nblk, int spj, const float* M, const float* denom,
+                         hipStream_t s);
 // blocksum[l][i][j] = sum_{p,q} dWe * W over joint block (i,j)
 void launch_wdot(const float* rg, const float* params, const int64_t* offs, const int* kin,
                  const int* nout, int nl, double* blocksum, hipStream_t s);

@@ -14,7 +14,10 @@ from lcn_amd.init import init_flat  # noqa: E402
 from tools.params_help import get_neighbour_matrix_by_hand  # noqa: E402
 from tools.filter_hub import neighbour_dict_set  # noqa: E402
 
-for knn, B in ((2, 200), (1, 512), (3, 4096)):
+CASES = ((2, 200), (1, 512), (3, 1024), (3, 2048), (3, 4096))
+if os.environ.get("SMALL_CASES"):  # e.g. "2:200,1:512"
+    CASES = tuple(tuple(int(v) for v in c.split(":")) for c in os.environ["SMALL_CASES"].split(","))
+for knn, B in CASES:
     nb = get_neighbour_matrix_by_hand(neighbour_dict_set[0], knn=knn)
     net = native.Network(F=64, in_F=2, num_layers=3, mask_type="locally_connected",
                          mask_matrix=(nb.T != 0).astype(np.float32), max_batch=B, device=0)
