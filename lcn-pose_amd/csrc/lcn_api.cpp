@@ -110,6 +110,7 @@ struct Handle {
   float* c123 = nullptr;
   float2* stat_part = nullptr;    // GEMM epilogue partials [tiles][H], tiles of stat_rows rows
   int stat_rows = kGemmRows;      // rows per partial of the last GEMM: 128, or 32 (small-batch kernel)
+  int small_rt = 0;               // launches of at most this many row tiles use the small-batch GEMM
   float2* col_part = nullptr;     // [B/kEwRows tiles][51] output-bias partials
   double2* colacc = nullptr;      // [kColSplit][H] float64 column sums
   float* dw_part = nullptr;
@@ -248,9 +249,8 @@ int dw_chunks(int nblk) {
 // splits every slab list over the four waves of a workgroup: measured faster
 // up to batch 1024 (0.92 -> 0.63 ms per step at batch 200, 1.24 -> 1.09 ms at
 // 1024), slower from 2048 on.  LCN_SMALL_RT overrides, 0 = never.
-int small_row_tiles() {
-  static const int t = std::getenv("LCN_SMALL_RT") ? std::atoi(std::getenv("LCN_SMALL_RT")) : 40;
-  return t;
+int small_row_tiles() {  // read when a handle is created
+  return std::getenv("LCN_SMALL_RT") ? std::atoi(std::getenv("LCN_SMALL_RT")) : 40;
 }
 
 // ---------------------------------------------------------------------------
@@ -258,6 +258,7 @@ int small_row_tiles() {
 // ---------------------------------------------------------------------------
 int build(Handle* h, const lcn_config* c) {
   if (const char* fp = std::getenv("LCN_FORCE_PHASED")) h->phased = std::atoi(fp) != 0;
+  h->small_rt = small_row_tiles();
   h->inF = c->in_f;
   h->F = c->f;
   h->L = c->num_layers;
@@ -513,7 +514,7 @@ int build(Handle* h, const lcn_config* c) {
   }
   CHECK(dalloc(h, &h->c123, 3 * F));
   CHECK(dalloc(h, &h->stat_part,
-               (size_t)std::max<int64_t>(cdiv(B, kGemmRows), std::min<int64_t>(cdiv(B, kRT), small_row_tiles())) * H));
+               (size_t)std::max<int64_t>(cdiv(B, kGemmRows), std::min<int64_t>(cdiv(B, kRT), h->small_rt)) * H));
   CHECK(dalloc(h, &h->col_part, (size_t)cdiv(B, kEwRows) * 64));
   CHECK(dalloc(h, &h->colacc, (size_t)kColSplit * H));
   h->loss_grid = (int)std::min<int64_t>(2048, cdiv(B, 4));
@@ -726,7 +727,7 @@ int gemm(Handle* h, const GemmCall& c, int B) {
   a.n_rt = (int)cdiv(B, kRT);
   // few row tiles: the kernel that splits the slab lists over a workgroup's
   // waves (no dropout epilogue there); its BN partials are per 32-row tile
-  const bool small = a.n_rt <= small_row_tiles() && !(c.epi_mode == EPI_BNBACK && a.epi_drop.rate > 0.f);
+  const bool small = a.n_rt <= h->small_rt && !(c.epi_mode == EPI_BNBACK && a.epi_drop.rate > 0.f);
   h->stat_rows = small ? kRT : kGemmRows;
   hipEvent_t ev[2];
   if (c.timer >= 0) tstart(h, c.timer, ev);

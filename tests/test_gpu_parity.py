@@ -25,9 +25,22 @@ CASES = [
     ("lc_nobn", dict(F=64, L=1, knn=2, batch_norm=False), 128),
     ("lc_noclip_reg", dict(F=64, L=1, knn=2, max_norm=False, regularization=0.01), 64),
     ("lc_tiny_B7", dict(F=64, L=1, knn=3), 7),
+    # 40 row tiles: the largest batch of the small-batch GEMM; 41: the first of the other
+    ("lc_B1280", dict(F=64, L=1, knn=2), 1280),
+    ("lc_B1290", dict(F=64, L=1, knn=2), 1290),
     # BASELINE.json configs[4] (cfg5) model shape: knn 5, 3 blocks
     ("cfg5_knn5_L3", dict(F=64, L=3, knn=5), 512),
 ]
+
+
+# Batches of up to 1280 rows run the small-batch GEMM kernel (gemm_small.hip);
+# LCN_SMALL_RT=0 at handle creation keeps such a batch on the large-batch
+# kernel (gemm_bs.hip), so both are held to the oracle on the same cases.
+@pytest.fixture(params=["small_batch_gemm", "large_batch_gemm"])
+def gemm_path(request, monkeypatch):
+    if request.param == "large_batch_gemm":
+        monkeypatch.setenv("LCN_SMALL_RT", "0")
+    return request.param
 
 
 def _setup(kw, B, seed=0):
@@ -40,7 +53,7 @@ def _setup(kw, B, seed=0):
 
 
 @pytest.mark.parametrize("name,kw,B", CASES, ids=[c[0] for c in CASES])
-def test_forward_matches_oracle(name, kw, B):
+def test_forward_matches_oracle(name, kw, B, gemm_path):
     cfg, params, x, lab, net = _setup(kw, B)
     out = net.forward(x)
     ref64, _ = O.forward(cfg, params, x, np.float64)
@@ -54,7 +67,7 @@ def test_forward_matches_oracle(name, kw, B):
 
 
 @pytest.mark.parametrize("name,kw,B", CASES, ids=[c[0] for c in CASES])
-def test_gradients_match_oracle(name, kw, B):
+def test_gradients_match_oracle(name, kw, B, gemm_path):
     cfg, params, x, lab, net = _setup(kw, B)
     loss, lr = net.train_step(x, lab, update=False, keep_grads=True)
     g = O.unflatten(cfg, net.get_grads())
@@ -78,7 +91,7 @@ def test_gradients_match_oracle(name, kw, B):
     np.testing.assert_array_equal(net.get_params(), O.flatten(cfg, params))
 
 
-def test_adam_step_matches_oracle():
+def test_adam_step_matches_oracle(gemm_path):
     cfg, params, x, lab, net = _setup(dict(F=64, L=2, knn=3), 256)
     st = O.adam_init(cfg, params)
     p_ref = {k: v.copy() for k, v in params.items()}
