@@ -33,7 +33,7 @@ struct SlabRegs {
 }  // namespace
 
 template <int PRO, int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_bs_small_kernel(GemmArgs a) {
+__global__ __launch_bounds__(256, 2) void gemm_bs_small_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) float red[3 * 2048];  // partial accumulators of waves 1..3
   __shared__ __attribute__((aligned(16))) float tab[4 * 64];    // epilogue constants (EPI_BNBACK)
   extern __shared__ __attribute__((aligned(16))) float dyn[];   // BN scale / shift of the operand (PRO_BNACT)

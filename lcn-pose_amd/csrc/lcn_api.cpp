@@ -247,10 +247,11 @@ int dw_chunks(int nblk) {
 
 // Launches of at most this many 32-row tiles run the small-batch kernel, which
 // splits every slab list over the four waves of a workgroup: measured faster
-// up to batch 1024 (0.92 -> 0.63 ms per step at batch 200, 1.24 -> 1.09 ms at
-// 1024), slower from 2048 on.  LCN_SMALL_RT overrides, 0 = never.
+// up to batch 2048 (0.92 -> 0.59 ms per step at batch 200, 1.24 -> 1.01 ms at
+// 1024, 1.48 -> 1.43 ms at 2048), slower from 2560 on (1.56 -> 1.57 ms; 4096:
+// 1.91 -> 2.11 ms).  LCN_SMALL_RT overrides, 0 = never.
 int small_row_tiles() {  // read when a handle is created
-  return std::getenv("LCN_SMALL_RT") ? std::atoi(std::getenv("LCN_SMALL_RT")) : 40;
+  return std::getenv("LCN_SMALL_RT") ? std::atoi(std::getenv("LCN_SMALL_RT")) : 72;
 }
 
 // ---------------------------------------------------------------------------
