@@ -400,15 +400,22 @@ def main(argv=None):
                       "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                       "frac_of_achievable": round(gbs / HBM_ACHIEVABLE_GBS, 4),
                       "achievable": HBM_ACHIEVABLE_GBS}
-        # the thin lift / output layers are HBM-bound too: algorithmic bytes =
-        # input rows read + output rows written
+        # the thin lift / output layers against HBM: algorithmic bytes = input
+        # rows read + output rows written.  Their narrow side is padded to the
+        # MFMA tile (34 -> 40 input features, 51 -> 64 output columns), which
+        # puts a matrix-core floor under each launch: mfma_floor_ms.
+        H = 17 * args.channels
+        kin = -(-17 * 2 // 8) * 8
+        pad_flops = {"lift": 2.0 * kin * H, "output": 2.0 * H * 64}
         hbm_thin = []
         for name, (nt, mst, bt) in thin_timing.items():
             if nt:
                 gbs = bt / (mst * 1e-3) / 1e9
+                fl = pad_flops["lift" if name.startswith("lift") else "output"] * B
                 hbm_thin.append({"kernel": name, "launches": nt, "avg_ms": round(mst / nt, 4),
                                  "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": round(gbs / HBM_PEAK_GBS, 4)})
+                                 "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                 "mfma_floor_ms": round(fl / (FP32_PEAK_TFLOPS * 1e12) * 1e3, 4)})
         hbm = None
         if "gemm_fwd" in kern:
             f = kern["gemm_fwd"]

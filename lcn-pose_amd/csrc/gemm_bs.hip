@@ -59,7 +59,9 @@ namespace lcn {
   {                                                                       \
     const float4* xs_ = xw + (size_t)(SI) * 512;                          \
     P##0 = xs_[0]; P##1 = xs_[64]; P##2 = xs_[128]; P##3 = xs_[192];      \
-    P##4 = xs_[256]; P##5 = xs_[320]; P##6 = xs_[384]; P##7 = xs_[448];   \
+    P##4 = xs_[256];                                                      \
+    if constexpr (KG > 5) { P##5 = xs_[320]; P##6 = xs_[384]; }           \
+    if constexpr (KG > 7) P##7 = xs_[448];                                \
   }
 // this thread's quarter of a weight block, global -> LDS buffer BUF by
 // LDS-DMA (global_load_lds_dwordx4: no VGPRs, no ds_write; each wave
@@ -70,7 +72,8 @@ namespace lcn {
   {                                                                       \
     const float4* ws_ = W4 + (size_t)(BLK) * 1024 + threadIdx.x;          \
     float4* d_ = Wl + (BUF) * 1024 + (threadIdx.x & ~63);                 \
-    GLDS(ws_, d_) GLDS(ws_ + 256, d_ + 256) GLDS(ws_ + 512, d_ + 512) GLDS(ws_ + 768, d_ + 768) \
+    GLDS(ws_, d_) GLDS(ws_ + 256, d_ + 256) GLDS(ws_ + 512, d_ + 512)     \
+    if constexpr (KG > 6) GLDS(ws_ + 768, d_ + 768)                       \
   }
 // BN apply + LeakyReLU of one activation fragment (k-group G of a slab whose
 // first channel is CH), scale / shift from the LDS tables
@@ -105,14 +108,19 @@ namespace lcn {
 #define COMPX(BUF, P, CH)                                                 \
   COMPX_PRE(P, CH)                                                        \
   GSTEP(BUF, 0, P##0, CH) GSTEP(BUF, 1, P##1, CH) GSTEP(BUF, 2, P##2, CH) \
-  GSTEP(BUF, 3, P##3, CH) GSTEP(BUF, 4, P##4, CH) GSTEP(BUF, 5, P##5, CH) \
-  GSTEP(BUF, 6, P##6, CH) GSTEP(BUF, 7, P##7, CH) SCHED_SLAB
+  GSTEP(BUF, 3, P##3, CH) GSTEP(BUF, 4, P##4, CH)                         \
+  if constexpr (KG > 5) { GSTEP(BUF, 5, P##5, CH) GSTEP(BUF, 6, P##6, CH) } \
+  if constexpr (KG > 7) { GSTEP(BUF, 7, P##7, CH) SCHED_SLAB }
 
 // EPI_BNBACK with the dropout of the layer below: a separate instance, since
 // the mask hash costs the plain kernel registers (it spilled)
 constexpr int kEpiBnBackDrop = 3;
 
-template <int PRO, int EPI>
+// KG: k-groups (8 features each) of an input slab that are multiplied.  8 for
+// the hidden layers; the lift's input slab holds 17 * in_F = 34 or 51 features
+// and zeros (its weight rows there are zero too), so its instances stop after
+// 5 or 7 groups: the thin layer is MFMA-bound at the padded width.
+template <int PRO, int EPI, int KG = 8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gemm_bs_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) float4 Wl[];  // [2][1024] (+ BN tables)
 #ifdef EXP_CLOCK
@@ -149,7 +157,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   const bool live = rt_raw < a.n_rt;
   // waves past the last row tile recompute it (they take part in the barriers)
   const int rt = live ? rt_raw : a.n_rt - 1;
-  const int beg = a.ptr[so], end = a.ptr[so + 1];
+  // the lift's lists are known without a load: output slab so <- block so of input slab 0
+  constexpr bool kLift = KG < 8;
+  const int beg = kLift ? 0 : a.ptr[so], end = kLift ? 1 : a.ptr[so + 1];
   const int2* __restrict__ idx = a.idx;
   const float4* __restrict__ W4 = (const float4*)a.blocks;
   const float4* xw = (const float4*)a.X + (size_t)rt * a.S_in * 512 + lane;
@@ -167,7 +177,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   const int tbase = (rt * S_out + so) * 512 + lane;
   DECLX(xa)
   DECLX(xb)
-  int2 ia = idx[beg], ib = ia;
+  int2 ia = kLift ? make_int2(0, so) : idx[beg], ib = ia;
   LOADW(ia.y, 0)
   LOADX(xa, ia.x)
   // accumulators start at bias + residual (the MFMAs add onto them)
@@ -439,7 +449,12 @@ void launch_gemm_bs(const GemmArgs& a, hipStream_t s) {
   const size_t ldse = lds + (256 + 4 * 64 * 3) * sizeof(float);
   const size_t ldsp = std::max(lds + 2 * a.pro_F * sizeof(float), ldse);
 #define LAUNCH(P, E, L) hipLaunchKernelGGL((gemm_bs_kernel<P, E>), dim3(grid), dim3(256), L, s, a)
-  if (a.pro_mode == PRO_BNACT) {
+#define LAUNCHK(P, E, K, L) hipLaunchKernelGGL((gemm_bs_kernel<P, E, K>), dim3(grid), dim3(256), L, s, a)
+  if (a.k_groups == 5 || a.k_groups == 7) {  // the lift: raw operand, BN statistics or none
+    const bool k5 = a.k_groups == 5;
+    if (a.epi_mode == EPI_BNFWD) { if (k5) LAUNCHK(PRO_RAW, EPI_BNFWD, 5, ldse); else LAUNCHK(PRO_RAW, EPI_BNFWD, 7, ldse); }
+    else { if (k5) LAUNCHK(PRO_RAW, EPI_NONE, 5, lds); else LAUNCHK(PRO_RAW, EPI_NONE, 7, lds); }
+  } else if (a.pro_mode == PRO_BNACT) {
     if (a.epi_mode == EPI_BNFWD) LAUNCH(PRO_BNACT, EPI_BNFWD, ldsp);
     else LAUNCH(PRO_BNACT, EPI_NONE, ldsp);
   } else {
@@ -449,6 +464,7 @@ void launch_gemm_bs(const GemmArgs& a, hipStream_t s) {
     else LAUNCH(PRO_RAW, EPI_NONE, lds);
   }
 #undef LAUNCH
+#undef LAUNCHK
 }
 
 }  // namespace lcn

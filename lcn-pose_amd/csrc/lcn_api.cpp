@@ -677,6 +677,7 @@ struct GemmCall {
   int epi_mode; int epi_layer;
   int timer; double flops_per_row;
   const int* order = nullptr;   // tail schedule (hidden layers); null: natural order
+  int k_groups = 0;             // non-zero 8-feature groups of the input slab (the lift), 0 = all
 };
 
 // row-tile groups per XCD issued longest-list-first at the end of a launch
@@ -699,6 +700,7 @@ int gemm(Handle* h, const GemmCall& c, int B) {
   a.idx = c.idx;
   a.order = c.order;
   a.tail = tail_groups();
+  a.k_groups = c.k_groups;
   a.bias = c.bias;
   a.pro_mode = c.X.mode;
   if (c.X.mode == PRO_BNACT) {
@@ -853,7 +855,8 @@ int forward(Handle* h, int B, bool with_labels, bool train) {
   // per row (input read + output written)
   const double lift_bytes = 4.0 * (kJ * h->inF + h->H), out_bytes = 4.0 * (h->H + 51);
   CHECK(gemm(h, GemmCall{raw(h->x, 1), h->wl[0].blk_fwd, h->thin_ptr, h->thin_idx, S,
-                         h->theta + h->b_off[0], h->Z[0], S, nullptr, epi, -1, LCN_K_LIFT, lift_bytes}, B));
+                         h->theta + h->b_off[0], h->Z[0], S, nullptr, epi, -1, LCN_K_LIFT, lift_bytes,
+                         nullptr, (int)cdiv(kJ * h->inF, 8)}, B));
   CHECK(bn_stats(h, 0, B));
   bn_act_timed(h, h->Z[0], nullptr, h->Hb[0], 0, B);
   // two_linear blocks (models_att.py:630-705)
