@@ -44,14 +44,6 @@ struct Timer {
 struct Handle {
   int device = 0;
   hipStream_t stream = nullptr;
-  // The chunk reduce of a weight gradient (dw_reduce) runs on a second stream
-  // beside the backward-data GEMM that follows it on `stream`: only the next
-  // weight-gradient GEMM (which overwrites the partials) and the end of the
-  // backward wait for it.  LCN_DW_SIDE=0 keeps it on `stream`.
-  hipStream_t side = nullptr;
-  hipEvent_t ev_dw = nullptr, ev_reduced = nullptr;
-  bool reduce_pending = false;
-  bool capturing = false;
   std::string err;
 
   // configuration
@@ -761,15 +753,6 @@ int gemm_hidden(Handle* h, int k, int kindt, const Operand& X, float* Y, const f
   return gemm(h, c, B);
 }
 
-// `stream` waits for the weight-gradient reduce in flight on the side stream
-int join_reduce(Handle* h) {
-  if (h->reduce_pending) {
-    HIPC(hipStreamWaitEvent(h->stream, h->ev_reduced, 0));
-    h->reduce_pending = false;
-  }
-  return LCN_OK;
-}
-
 // dW_e of a layer from A (input activations, raw or BN-apply prologue) and D
 // (raw, or dz rebuilt from (dh, z) by the BN backward prologue -- then also
 // stored to dz_out when given): partial slabs per batch chunk, then a
@@ -812,22 +795,11 @@ int gemm_dw(Handle* h, const Operand& A, const Operand& D, const int2* blk, int 
   a.nchunks = (int)cdiv(B, a.chunk_rows);
   a.part = h->dw_part;
   hipEvent_t ev[2];
-  CHECK(join_reduce(h));  // the previous reduce has read the partials this launch overwrites
   if (timer >= 0) tstart(h, timer, ev);
   launch_gemm_dw(a, h->stream);
   if (timer >= 0)
     tstop(h, timer, ev, timer == LCN_K_GEMM_DW ? 2.0 * 4096.0 * nblk * B : 4.0 * (h->H + 51) * (double)B);
-  hipStream_t rs = h->stream;
-  if (h->side && !h->capturing) {
-    HIPC(hipEventRecord(h->ev_dw, h->stream));
-    HIPC(hipStreamWaitEvent(h->side, h->ev_dw, 0));
-    rs = h->side;
-  }
-  launch_dw_reduce(h->dw_part, a.nchunks, nblk, blk, dW, ld, rows_valid, cols_valid, rs);
-  if (rs != h->stream) {
-    HIPC(hipEventRecord(h->ev_reduced, rs));
-    h->reduce_pending = true;
-  }
+  launch_dw_reduce(h->dw_part, a.nchunks, nblk, blk, dW, ld, rows_valid, cols_valid, h->stream);
   return LCN_OK;
 }
 
@@ -967,7 +939,7 @@ int backward(Handle* h, int B) {
   CHECK(bn_back(h, 0, B));
   CHECK(gemm_dw(h, raw(h->x, 1), Operand{h->DH, S, PRO_BNBACK, 0}, h->lift_blk, S,
                 h->rg + h->wl[0].w_off, H, kJ * h->inF, H, B, -1));
-  return join_reduce(h);  // the raw-gradient vector is complete on `stream`
+  return LCN_OK;
 }
 
 // the device side of the update: mask / clip backward, Adam (lr_t from lr_dev)
@@ -1039,10 +1011,6 @@ int lcn_create(const lcn_config* c, int device, void** handle) {
   h->device = device;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
-  const bool side_on = !(std::getenv("LCN_DW_SIDE") && std::atoi(std::getenv("LCN_DW_SIDE")) == 0);
-  if (e == hipSuccess && side_on) e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
-  if (e == hipSuccess && side_on) e = hipEventCreateWithFlags(&h->ev_dw, hipEventDisableTiming);
-  if (e == hipSuccess && side_on) e = hipEventCreateWithFlags(&h->ev_reduced, hipEventDisableTiming);
   if (e != hipSuccess) {
     g_create_error = std::string("HIP init: ") + hipGetErrorString(e);
     delete h;
@@ -1067,7 +1035,6 @@ int lcn_destroy(void* handle) {
   Handle* h = (Handle*)handle;
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
-  if (h->side) hipStreamSynchronize(h->side);
   if (h->comm) ncclCommDestroy(h->comm);
   for (auto& t : h->timers)
     for (auto e : t.ev) hipEventDestroy(e);
@@ -1078,9 +1045,6 @@ int lcn_destroy(void* handle) {
   if (h->pred) hipFree(h->pred);
   if (h->pred_out) hipFree(h->pred_out);
   if (h->batch_losses) hipFree(h->batch_losses);
-  if (h->ev_dw) hipEventDestroy(h->ev_dw);
-  if (h->ev_reduced) hipEventDestroy(h->ev_reduced);
-  if (h->side) hipStreamDestroy(h->side);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return LCN_OK;
@@ -1232,9 +1196,7 @@ static int step_graph(Handle* h, int64_t B, bool update, bool keep, hipGraphExec
     if (g.B == B && g.update == update && g.keep == keep) { *out = g.exec; return LCN_OK; }
   hipGraph_t graph = nullptr;
   HIPC(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
-  h->capturing = true;  // one stream only inside a captured step
   const int rc = enqueue_step(h, B, update, keep);
-  h->capturing = false;
   const hipError_t ec = hipStreamEndCapture(h->stream, &graph);
   if (rc != LCN_OK) { if (graph) hipGraphDestroy(graph); return rc; }
   if (ec != hipSuccess) { h->err = std::string("step graph capture: ") + hipGetErrorString(ec); return LCN_E_HIP; }
