@@ -6,7 +6,7 @@ WRITE_SIZE is exact for 16-B stores.  Both counters are in KiB.  Launch
 classes follow bench.py's timer categories: gemm_dw = the hidden-layer
 weight-gradient launches (the largest dW grid), gemm_fwd = forward launches
 of the hidden layers (gemm_bs_kernel<*, 1> with the largest grid), gemm_dx =
-gemm_bs_kernel<0, 2> with the largest grid.
+gemm_bs_kernel<0, 2, *> with the largest grid.
 """
 import collections
 import csv
@@ -29,7 +29,8 @@ def classify(name):
     if "gemm_dw_kernel" in name:
         return "gemm_dw"
     if "gemm_bs_kernel" in name:
-        if name.split("<")[1].split(">")[0].replace(" ", "").endswith(",2"):
+        targs = name.split("<")[1].split(">")[0].replace(" ", "").split(",")
+        if len(targs) > 1 and targs[1] in ("2", "3"):  # <PRO, EPI, KG>: EPI_BNBACK (3: with dropout)
             return "gemm_dx"
         return "gemm_fwd"
     return None
