@@ -70,14 +70,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   [[maybe_unused]] Dropout dr{};
   if constexpr (DROP) dr = drop_resolve(a.d_drop);
 
-  // this thread's staging slots: j = 0, 1 -> chunk g = w + 4j of the stage's
-  // row tile, lane `lane`: row lr, features f0 + 32j .. +3
+  // this thread's staging slots: the same four features f0 .. f0 + 3 of two
+  // rows, sr and sr + 16, of the stage's row tile (float4 c40, c40 + 16 of the
+  // slab: chunk g = t >> 5, lane half (t >> 4) & 1) -- one set of channel
+  // constants serves both
   const float4* A4 = (const float4*)a.A;
   const float4* D4 = (const float4*)a.D;
   const float4* Z4 = (const float4*)a.d_z;
   const int S_a = a.S_a, S_d = a.S_d;
-  const int c40 = t, c41 = t + 256;
-  const int f0 = 8 * w + 4 * h;
+  const int sr = t & 15;
+  const int c40 = (t >> 5) * 64 + ((t >> 4) & 1) * 32 + sr, c41 = c40 + 16;
+  const int f0 = 8 * (t >> 5) + 4 * ((t >> 4) & 1);
   float4 ra0, ra1, rb0, rb1, rd0, rd1, rz0, rz1;
 #define DW_IX(RT, S, SL, C4) (((size_t)(RT) * (S) + (SL)) * 512 + (C4))
 #define DW_GLOAD(BASE)                                                     \
@@ -99,47 +102,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   if (r0 < r1) DW_GLOAD(r0);
   for (int base = r0; base < r1; base += kRT) {
     __syncthreads();  // previous stage's fragment reads are done (and the tables written)
-    const bool v = base + lr < r1;
+    const bool v0 = base + sr < r1, v1 = base + sr + 16 < r1;
     if constexpr (PRO) {
-      ra0 = bnact4(ra0, *(const float4*)(tab + f0), *(const float4*)(tab + 64 + f0), a.alpha);
-      ra1 = bnact4(ra1, *(const float4*)(tab + f0 + 32), *(const float4*)(tab + 96 + f0), a.alpha);
+      const float4 sc0 = *(const float4*)(tab + f0), sh0 = *(const float4*)(tab + 64 + f0);
+      ra0 = bnact4(ra0, sc0, sh0, a.alpha);
+      ra1 = bnact4(ra1, sc0, sh0, a.alpha);
       if (two) {
-        rb0 = bnact4(rb0, *(const float4*)(tab + 128 + f0), *(const float4*)(tab + 192 + f0), a.alpha);
-        rb1 = bnact4(rb1, *(const float4*)(tab + 160 + f0), *(const float4*)(tab + 224 + f0), a.alpha);
+        const float4 sc1 = *(const float4*)(tab + 128 + f0), sh1 = *(const float4*)(tab + 192 + f0);
+        rb0 = bnact4(rb0, sc1, sh1, a.alpha);
+        rb1 = bnact4(rb1, sc1, sh1, a.alpha);
       }
     }
     if constexpr (DBB) {
-      auto coef = [&](int f) {
-        BnBackCoef c;
-        c.sc = *(const float4*)(tab + 256 + f); c.sh = *(const float4*)(tab + 320 + f);
-        c.c1 = *(const float4*)(tab + 384 + f); c.c2 = *(const float4*)(tab + 448 + f);
-        c.c3 = *(const float4*)(tab + 512 + f);
-        return c;
-      };
+      BnBackCoef cf;
+      cf.sc = *(const float4*)(tab + 256 + f0); cf.sh = *(const float4*)(tab + 320 + f0);
+      cf.c1 = *(const float4*)(tab + 384 + f0); cf.c2 = *(const float4*)(tab + 448 + f0);
+      cf.c3 = *(const float4*)(tab + 512 + f0);
       if constexpr (DROP) {  // tf.nn.dropout's gradient: dh * mask * scale
-        const int64_t row = base + lr;
+        const int64_t row = base + sr;
         const int col = so * kSlab + f0;
         rd0.x = drop_apply(dr, row, col, rd0.x);
         rd0.y = drop_apply(dr, row, col + 1, rd0.y);
         rd0.z = drop_apply(dr, row, col + 2, rd0.z);
         rd0.w = drop_apply(dr, row, col + 3, rd0.w);
-        rd1.x = drop_apply(dr, row, col + 32, rd1.x);
-        rd1.y = drop_apply(dr, row, col + 33, rd1.y);
-        rd1.z = drop_apply(dr, row, col + 34, rd1.z);
-        rd1.w = drop_apply(dr, row, col + 35, rd1.w);
+        rd1.x = drop_apply(dr, row + 16, col, rd1.x);
+        rd1.y = drop_apply(dr, row + 16, col + 1, rd1.y);
+        rd1.z = drop_apply(dr, row + 16, col + 2, rd1.z);
+        rd1.w = drop_apply(dr, row + 16, col + 3, rd1.w);
       }
-      rd0 = bnback4(rd0, rz0, coef(f0), a.alpha);
-      rd1 = bnback4(rd1, rz1, coef(f0 + 32), a.alpha);
-      if (writer && v) {
+      rd0 = bnback4(rd0, rz0, cf, a.alpha);
+      rd1 = bnback4(rd1, rz1, cf, a.alpha);
+      if (writer) {
         float4* o = (float4*)a.dz_out;
         const int t_ = base / kRT;
-        o[DW_IX(t_, S_d, so, c40)] = rd0;
-        o[DW_IX(t_, S_d, so, c41)] = rd1;
+        if (v0) o[DW_IX(t_, S_d, so, c40)] = rd0;
+        if (v1) o[DW_IX(t_, S_d, so, c41)] = rd1;
       }
     }
-    if (!v) {  // rows past the chunk end contribute nothing
+    {  // rows past the chunk end contribute nothing
       const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      ra0 = z4; ra1 = z4; rb0 = z4; rb1 = z4; rd0 = z4; rd1 = z4;
+      if (!v0) { ra0 = z4; rb0 = z4; rd0 = z4; }
+      if (!v1) { ra1 = z4; rb1 = z4; rd1 = z4; }
     }
     {
       // transposed scatter: feature -> LDS row, batch row -> column
@@ -148,7 +151,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   P[(OFF) + kDwLd] = (F4).y;           \
   P[(OFF) + 2 * kDwLd] = (F4).z;       \
   P[(OFF) + 3 * kDwLd] = (F4).w;
-      const int o0 = f0 * kDwLd + lr, o1 = o0 + 32 * kDwLd;
+      const int o0 = f0 * kDwLd + sr, o1 = o0 + 16;
       DW_PUT(As[0], ra0, o0) DW_PUT(As[0], ra1, o1)
       if (two) { DW_PUT(As[1], rb0, o0) DW_PUT(As[1], rb1, o1) }
       DW_PUT(Ds, rd0, o0) DW_PUT(Ds, rd1, o1)
