@@ -83,9 +83,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   const int f0 = 8 * (t >> 5) + 4 * ((t >> 4) & 1);
   float4 ra0, ra1, rb0, rb1, rd0, rd1, rz0, rz1;
 #define DW_IX(RT, S, SL, C4) (((size_t)(RT) * (S) + (SL)) * 512 + (C4))
+#ifdef EXP_DW_HOT  // diagnostic build: every stage reads one of four row tiles (operands stay in L2)
+#define DW_TILE(BASE) (((BASE) / kRT) & 3)
+#else
+#define DW_TILE(BASE) ((BASE) / kRT)
+#endif
 #define DW_GLOAD(BASE)                                                     \
   {                                                                        \
-    const int t_ = (BASE) / kRT;                                           \
+    const int t_ = DW_TILE(BASE);                                          \
     ra0 = A4[DW_IX(t_, S_a, si0, c40)];                                    \
     ra1 = A4[DW_IX(t_, S_a, si0, c41)];                                    \
     if (two) {                                                             \
@@ -197,6 +202,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
     __builtin_amdgcn_s_setprio(0);
   }
 #undef DW_GLOAD
+#undef DW_TILE
 #undef DW_IX
   if (two) {
     float* out = a.part + ((size_t)chunk * a.nblk + (bi ? b1 : b0)) * 4096;
