@@ -63,23 +63,28 @@ __global__ __launch_bounds__(256) void wnorm_part_kernel(const float* __restrict
   if (threadIdx.x == 0) part[l * ppl + p] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ void wnorm_final_kernel(const double* __restrict__ part, int ppl, int nl,
-                                   double* __restrict__ norm2, float* __restrict__ denom,
-                                   int max_norm) {
+// one wave per entry: lane i adds partials i, i + 64, ... in order, then a
+// fixed butterfly over the lanes (deterministic)
+__global__ __launch_bounds__(64) void wnorm_final_kernel(const double* __restrict__ part, int ppl, int nl,
+                                                         double* __restrict__ norm2, float* __restrict__ denom,
+                                                         int max_norm) {
   // entries [0, nl/2) are weights (clip denominators); the rest only get norm2
-  const int l = threadIdx.x;
-  if (l >= nl) return;
+  const int l = blockIdx.x, lane = threadIdx.x;
   double s = 0.0;
-  for (int p = 0; p < ppl; ++p) s += part[l * ppl + p];
-  norm2[l] = s;
-  if (l < nl / 2) denom[l] = max_norm ? fmaxf((float)sqrt(s), 1.0f) : 1.0f;
+  for (int p = lane; p < ppl; p += 64) s += part[l * ppl + p];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0) {
+    norm2[l] = s;
+    if (l < nl / 2) denom[l] = max_norm ? fmaxf((float)sqrt(s), 1.0f) : 1.0f;
+  }
 }
 
 void launch_wnorm(const float* params, const int64_t* offs, const int64_t* sizes, int nl,
                   double* part, int ppl, double* norm2, float* denom, int max_norm, hipStream_t s) {
   hipLaunchKernelGGL(wnorm_part_kernel, dim3(ppl, nl), dim3(256), 0, s, params, offs, sizes, part,
                      ppl);
-  hipLaunchKernelGGL(wnorm_final_kernel, dim3(1), dim3(64), 0, s, part, ppl, nl, norm2, denom,
+  hipLaunchKernelGGL(wnorm_final_kernel, dim3(nl), dim3(64), 0, s, part, ppl, nl, norm2, denom,
                      max_norm);
 }
 
@@ -213,16 +218,23 @@ __global__ __launch_bounds__(320) void maskgrad_kernel(const double* __restrict_
                                                        float* __restrict__ lcoef) {
   __shared__ double dS[kJ * kJ];
   const int t = threadIdx.x;
-  if (t < nl) {
+  // one wave per layer: lane i adds entries i, i + 64, ..., then a fixed
+  // butterfly over the lanes (deterministic)
+  for (int l = t >> 6; l < nl; l += 320 / 64) {
+    const int lane = t & 63;
     double dot = 0.0;
-    for (int e = 0; e < kJ * kJ; ++e) dot += (double)M[e] * bs[t * kJ * kJ + e];
-    const double n = sqrt(norm2[t]);
-    if (max_norm && n > 1.0) {
-      lcoef[2 * t] = (float)(1.0 / n);
-      lcoef[2 * t + 1] = (float)(dot / (n * n * n));
-    } else {
-      lcoef[2 * t] = 1.f;
-      lcoef[2 * t + 1] = 0.f;
+    for (int e = lane; e < kJ * kJ; e += 64) dot += (double)M[e] * bs[l * kJ * kJ + e];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dot += __shfl_xor(dot, off);
+    if (lane == 0) {
+      const double n = sqrt(norm2[l]);
+      if (max_norm && n > 1.0) {
+        lcoef[2 * l] = (float)(1.0 / n);
+        lcoef[2 * l + 1] = (float)(dot / (n * n * n));
+      } else {
+        lcoef[2 * l] = 1.f;
+        lcoef[2 * l + 1] = 0.f;
+      }
     }
   }
   if (!learnable) return;
