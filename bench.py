@@ -324,7 +324,15 @@ def main(argv=None):
     for _ in range(args.warmup):
         net.train_step_device(xb.ptr, lb.ptr, B)
     barrier()
-    net.set_timing(True)
+    # Timed region: HIP-event timers (on the library's compute stream) around
+    # the roofline's kernel only, the hidden-layer weight-gradient GEMM (the
+    # largest share of the step; checked against the other classes below).
+    # Every timed launch adds two event records to the stream -- timing all
+    # classes costs 0.4 % of the step -- so the other classes are timed in a
+    # second pass over the same steps that `value` does not include.
+    gemm_ids = (("gemm_fwd", native.K_GEMM_FWD), ("gemm_dx", native.K_GEMM_DX),
+                ("gemm_dw", native.K_GEMM_DW))
+    net.set_timing(True, only=[native.K_GEMM_DW])
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -334,12 +342,22 @@ def main(argv=None):
     elapsed = time.perf_counter() - t0
     elapsed = float(net.allreduce_host([elapsed], op="max")[0])
     kern = {}
-    for name, kid in (("gemm_fwd", native.K_GEMM_FWD), ("gemm_dx", native.K_GEMM_DX),
-                      ("gemm_dw", native.K_GEMM_DW)):
-        n, ms, fl = net.kernel_timing(kid)
-        if n:
-            kern[name] = {"launches": n, "avg_ms": ms / n, "tflops": fl / (ms * 1e-3) / 1e12,
-                          "total_ms_per_step": ms / args.steps}
+
+    def read_kernels(ids, where):
+        for name, kid in ids:
+            n, ms, fl = net.kernel_timing(kid)
+            if n:
+                kern[name] = {"launches": n, "avg_ms": ms / n, "tflops": fl / (ms * 1e-3) / 1e12,
+                              "total_ms_per_step": ms / args.steps, "timed_in": where}
+
+    read_kernels(gemm_ids[2:], "timed region")
+    net.set_timing(True, only=[native.K_GEMM_FWD, native.K_GEMM_DX, native.K_BN_ACT, native.K_LIFT,
+                               native.K_OUT, native.K_OUT_DW])
+    for _ in range(args.steps):
+        net.train_step_device(xb.ptr, lb.ptr, B)
+    net.synchronize()
+    barrier()
+    read_kernels(gemm_ids[:2], "second pass")
     bn_act_timing = net.kernel_timing(native.K_BN_ACT)
     thin_timing = {name: net.kernel_timing(kid) for name, kid in (
         ("lift (x . W1e + b1, BN statistics)", native.K_LIFT),
@@ -378,7 +396,10 @@ def main(argv=None):
         dom = max(kern, key=lambda k: kern[k]["total_ms_per_step"])
         d = kern[dom]
         traffic = None
-        if os.path.exists(args.traffic_file):
+        # the committed PMC traffic was collected on the cfg3 workload at 65 536 rows
+        pmc_applies = (B == 65536 and args.channels == 64 and args.knn == 3 and args.layers == 3
+                       and args.mask_type == "locally_connected")
+        if pmc_applies and os.path.exists(args.traffic_file):
             try:
                 traffic = json.load(open(args.traffic_file)).get(dom, {}).get("hbm_bytes_per_launch")
             except Exception:
@@ -386,7 +407,7 @@ def main(argv=None):
         roof = {"bound": "mfma", "kernel": f"{dom} (block-sparse fp32 v_mfma_f32_32x32x2_f32)",
                 "achieved": round(d["tflops"], 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(d["tflops"] / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-                "avg_launch_ms": round(d["avg_ms"], 4)}
+                "avg_launch_ms": round(d["avg_ms"], 4), "timed_in": d["timed_in"]}
         # the metric's "achieved HBM GB/s vs peak", for the hidden-layer forward
         # GEMM (the north star's fused LCN forward): algorithmic bytes = read the
         # input activations + write z, 2 x 17*F floats per pose
@@ -421,7 +442,7 @@ def main(argv=None):
             f = kern["gemm_fwd"]
             alg = 2 * 17 * args.channels * 4 * B
             tr = None
-            if os.path.exists(args.traffic_file):
+            if pmc_applies and os.path.exists(args.traffic_file):
                 try:
                     tr = json.load(open(args.traffic_file)).get("gemm_fwd", {}).get("hbm_bytes_per_launch")
                 except Exception:

@@ -577,15 +577,17 @@ int exchange_rows(Handle* h, int64_t B) {
 // (then the by-value local row count is the global one)
 const RowInfo* rinfo(const Handle* h) { return multi(h) ? h->rowinfo : nullptr; }
 
+// lcn_set_timing: 1 = every kernel class, else bit k + 1 selects class k
+bool timed(const Handle* h, int k) { return h->timing == 1 || ((h->timing >> (k + 1)) & 1); }
+
 void tstart(Handle* h, int k, hipEvent_t* pair) {
-  if (!h->timing) return;
+  if (!timed(h, k)) return;
   hipEventCreate(&pair[0]);
   hipEventCreate(&pair[1]);
   hipEventRecord(pair[0], h->stream);
-  (void)k;
 }
 void tstop(Handle* h, int k, hipEvent_t* pair, double flops) {
-  if (!h->timing) return;
+  if (!timed(h, k)) return;
   hipEventRecord(pair[1], h->stream);
   h->timers[k].ev.push_back(pair[0]);
   h->timers[k].ev.push_back(pair[1]);

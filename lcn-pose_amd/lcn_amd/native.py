@@ -420,8 +420,13 @@ class Network:
         The step counter of the masks restarts at 0."""
         self._check(self.lib.lcn_set_dropout(self.h, float(rate), int(seed) & (2 ** 64 - 1)))
 
-    def set_timing(self, enable: bool):
-        self._check(self.lib.lcn_set_timing(self.h, int(enable)))
+    def set_timing(self, enable, only=None):
+        """HIP-event timers around the kernel classes K_*: all of them, or
+        only the classes listed in `only`; resets the accumulated timings."""
+        flags = int(bool(enable))
+        if enable and only is not None:
+            flags = sum(1 << (1 + k) for k in only)
+        self._check(self.lib.lcn_set_timing(self.h, flags))
 
     def kernel_timing(self, kernel: int):
         n, ms, fl = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
