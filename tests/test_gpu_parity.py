@@ -339,3 +339,28 @@ def test_step_graphs_replay_the_direct_launches(monkeypatch):
     s0, s1 = nets[0].get_optimizer_state(), nets[1].get_optimizer_state()
     for a, b in zip(s0, s1):
         np.testing.assert_array_equal(a, b)
+
+
+def test_timers_cover_the_selected_kernel_classes_only():
+    """lcn_set_timing with a set of classes: only those launches are timed,
+    and the timers change nothing in the step's result."""
+    from lcn_amd import native
+    L, B = 2, 4096  # above the small-batch GEMM limit: the large kernels, colreduce path
+    cfg, params, x, lab, net = _setup(dict(F=64, L=L, knn=3), B, seed=3)
+    loss0, _ = net.train_step(x, lab, update=False)
+    net.set_timing(True, only=[native.K_GEMM_DW, native.K_LIFT])
+    loss1, _ = net.train_step(x, lab, update=False)
+    n_dw, ms_dw, fl_dw = net.kernel_timing(native.K_GEMM_DW)
+    assert n_dw == 2 * L and ms_dw > 0 and fl_dw == 2 * L * 2.0 * 4096.0 * 175 * B
+    assert net.kernel_timing(native.K_LIFT)[0] == 1
+    for k in (native.K_GEMM_FWD, native.K_GEMM_DX, native.K_BN_ACT, native.K_OUT, native.K_OUT_DW):
+        assert net.kernel_timing(k)[0] == 0, k
+    net.set_timing(True)
+    net.train_step(x, lab, update=False)
+    assert net.kernel_timing(native.K_GEMM_FWD)[0] == 2 * L
+    assert net.kernel_timing(native.K_GEMM_DX)[0] == 2 * L
+    net.set_timing(False)
+    net.train_step(x, lab, update=False)
+    assert net.kernel_timing(native.K_GEMM_DW)[0] == 0
+    assert loss1 == loss0
+    net.close()
