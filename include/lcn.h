@@ -247,8 +247,8 @@ uint32_t lcn_crc32c(uint32_t crc, const void* data, int64_t n);
 enum { LCN_K_GEMM_FWD = 0, LCN_K_GEMM_DX = 1, LCN_K_GEMM_DW = 2, LCN_K_BN_ACT = 3, LCN_K_LIFT = 4,
        LCN_K_OUT = 5, LCN_K_OUT_DW = 6, LCN_K_NUM = 7 };
 /* enable: 0 = off, 1 = HIP-event timers around every kernel class above, or a
- * set of bits 1 << (1 + LCN_K_x) to time only those classes (each timed launch
- * adds two event records to the stream).  Resets the accumulated timings. */
+ * set of bits 1 << (1 + LCN_K_x) to time only those classes (timing-only
+ * events: two records per timed launch, no system fence).  Resets the accumulated timings. */
 int lcn_set_timing(void* handle, int32_t enable);
 int lcn_kernel_timing(void* handle, int32_t kernel, int64_t* launches, double* total_ms,
                       double* flops);

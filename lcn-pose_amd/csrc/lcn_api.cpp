@@ -582,8 +582,9 @@ bool timed(const Handle* h, int k) { return h->timing == 1 || ((h->timing >> (k 
 
 void tstart(Handle* h, int k, hipEvent_t* pair) {
   if (!timed(h, k)) return;
-  hipEventCreate(&pair[0]);
-  hipEventCreate(&pair[1]);
+  // timing-only events: no system-scope fence when they complete
+  hipEventCreateWithFlags(&pair[0], hipEventDisableSystemFence);
+  hipEventCreateWithFlags(&pair[1], hipEventDisableSystemFence);
   hipEventRecord(pair[0], h->stream);
 }
 void tstop(Handle* h, int k, hipEvent_t* pair, double flops) {
