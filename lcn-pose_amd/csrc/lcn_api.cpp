@@ -238,11 +238,18 @@ int upload_dw_groups(Handle* h, const std::vector<int2>& blk, int4** dev, int* n
 }
 
 // batch chunks of a weight-gradient launch (partials per block = chunks);
-// LCN_DW_ROWS overrides the block-rows budget (tuning runs)
-int dw_chunks(int nblk) {
+// LCN_DW_ROWS / LCN_DW_MAXCH / LCN_DW_MINCH override the block-rows budget and the limits (tuning runs)
+int dw_chunks(int nblk, int64_t B) {
   static const int budget = std::getenv("LCN_DW_ROWS") ? std::atoi(std::getenv("LCN_DW_ROWS")) : 5600;
   static const int cap = std::getenv("LCN_DW_MAXCH") ? std::atoi(std::getenv("LCN_DW_MAXCH")) : 64;
-  return std::max(1, std::min(cap, budget / std::max(1, nblk)));
+  // At least 16 chunks, and chunks of at most 2048 rows: with many blocks
+  // (F >= 128: 4 624 at the cfg4 shape) one chunk per block leaves 2.3 rounds of
+  // long workgroups and a third of the last round idle (cfg4 shape, 16 384 rows
+  // per GPU, same box: 1 / 4 / 8 / 16 chunks 6.05 / 5.61 / 5.85 / 5.37 ms per
+  // launch; 24 / 32 / 64 slower again)
+  static const int lo = std::getenv("LCN_DW_MINCH") ? std::atoi(std::getenv("LCN_DW_MINCH")) : 16;
+  const int by_rows = (int)std::min<int64_t>(cap, B / 2048);
+  return std::max(std::max(lo, by_rows), std::min(cap, budget / std::max(1, nblk)));
 }
 
 // Launches of at most this many 32-row tiles run the small-batch kernel, which
@@ -524,8 +531,8 @@ int build(Handle* h, const lcn_config* c) {
   CHECK(dalloc(h, &h->acc1, 2 * F));
   CHECK(dalloc(h, &h->acc2, 2 * F));
   CHECK(dalloc(h, &h->rowinfo, 1));
-  const size_t dw_elems = std::max((size_t)dw_chunks(h->nblk) * h->nblk,
-                                   (size_t)dw_chunks(h->nslab) * h->nslab) * 4096;
+  const size_t dw_elems = std::max((size_t)dw_chunks(h->nblk, B) * h->nblk,
+                                   (size_t)dw_chunks(h->nslab, B) * h->nslab) * 4096;
   CHECK(dalloc(h, &h->dw_part, dw_elems));
   return LCN_OK;
 }
@@ -793,7 +800,7 @@ int gemm_dw(Handle* h, const Operand& A, const Operand& D, const int2* blk, int 
   else if (blk == h->out_blk) { a.groups = h->grp_out; a.ngroups = h->ngrp_out; }
   else { h->err = "internal: unknown block list"; return LCN_E_ARG; }
   a.B = B;
-  const int nch = std::max(1, std::min<int>(dw_chunks(nblk), (int)cdiv(B, 64)));
+  const int nch = std::max(1, std::min<int>(dw_chunks(nblk, B), (int)cdiv(B, 64)));
   a.chunk_rows = (int)(cdiv(cdiv(B, nch), 64) * 64);
   a.nchunks = (int)cdiv(B, a.chunk_rows);
   a.part = h->dw_part;
