@@ -159,6 +159,7 @@ int main(int argc, char** argv) {
     a.n_out_slabs = J;
     a.n_rt = (B + kRT - 1) / kRT;
     (void)variant;
+    a.n_blocks = nblk;
     return a;
   };
   GemmDwArgs d{};

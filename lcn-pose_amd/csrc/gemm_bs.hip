@@ -54,26 +54,40 @@ namespace lcn {
   acc1 = MFMA32((W1).w, (XV).w, acc1);
 
 #define DECLX(P) float4 P##0, P##1, P##2, P##3, P##4, P##5, P##6, P##7;
-// activation fragments of input slab si (8 chunks of this wave's row tile)
+// Operand loads are BUFFER loads: a scalar resource (base + size) with one
+// 32-bit offset register per lane, the slab / block part of the address in
+// scalar registers.  Beside a stream of MFMAs a load that takes a 64-bit address
+// pair per lane costs matrix-core time (scripts/microbench/mfma_steps.hip: the
+// slab loop's 12 loads per 64 MFMAs 83.7 % of the MFMA peak as global loads,
+// 88.4 % as buffer loads, all L2 hits); reads past a resource return 0.
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+#define BUFLD(RES, VOFF, SOFF)                                                         \
+  ({                                                                                   \
+    const v4f_t v_ = __builtin_bit_cast(v4f_t, __builtin_amdgcn_raw_buffer_load_b128((RES), (VOFF), (SOFF), 0)); \
+    make_float4(v_.x, v_.y, v_.z, v_.w);                                               \
+  })
+// activation fragments of input slab si (8 chunks of this wave's row tile):
+// byte offset si * 8192 + chunk * 1024 (scalar) + lane * 16
 #define LOADX(P, SI)                                                      \
   {                                                                       \
-    const float4* xs_ = xw + (size_t)(SI) * 512;                          \
-    P##0 = xs_[0]; P##1 = xs_[64]; P##2 = xs_[128]; P##3 = xs_[192];      \
-    P##4 = xs_[256];                                                      \
-    if constexpr (KG > 5) { P##5 = xs_[320]; P##6 = xs_[384]; }           \
-    if constexpr (KG > 7) P##7 = xs_[448];                                \
+    const int so_ = (SI) * 8192;                                          \
+    P##0 = BUFLD(xres, xlo, so_);          P##1 = BUFLD(xres, xlo + 1024, so_); \
+    P##2 = BUFLD(xres, xlo + 2048, so_);   P##3 = BUFLD(xres, xlo + 3072, so_); \
+    P##4 = BUFLD(xres, xlo, so_ + 4096);                                  \
+    if constexpr (KG > 5) { P##5 = BUFLD(xres, xlo + 1024, so_ + 4096); P##6 = BUFLD(xres, xlo + 2048, so_ + 4096); } \
+    if constexpr (KG > 7) P##7 = BUFLD(xres, xlo + 3072, so_ + 4096);     \
   }
 // this thread's quarter of a weight block, global -> LDS buffer BUF by
-// LDS-DMA (global_load_lds_dwordx4: no VGPRs, no ds_write; each wave
+// LDS-DMA (buffer_load_dwordx4 ... lds: no VGPRs, no ds_write; each wave
 // instruction lands 1 KB lane-linear, which is the fragment-packed order)
-#define GLDS(SRC, DST) \
-  __builtin_amdgcn_global_load_lds((const void*)(SRC), (__attribute__((address_space(3))) void*)(DST), 16, 0, 0);
+#define GLDS(SOFF, DST) \
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(wres, (__attribute__((address_space(3))) void*)(DST), 16, wlo, (SOFF), 0, 0);
 #define LOADW(BLK, BUF)                                                   \
   {                                                                       \
-    const float4* ws_ = W4 + (size_t)(BLK) * 1024 + threadIdx.x;          \
+    const int bo_ = (BLK) * 16384;                                        \
     float4* d_ = Wl + (BUF) * 1024 + (threadIdx.x & ~63);                 \
-    GLDS(ws_, d_) GLDS(ws_ + 256, d_ + 256) GLDS(ws_ + 512, d_ + 512)     \
-    if constexpr (KG > 6) GLDS(ws_ + 768, d_ + 768)                       \
+    GLDS(bo_, d_) GLDS(bo_ + 4096, d_ + 256) GLDS(bo_ + 8192, d_ + 512)   \
+    if constexpr (KG > 6) GLDS(bo_ + 12288, d_ + 768)                     \
   }
 // BN apply + LeakyReLU of one activation fragment (k-group G of a slab whose
 // first channel is CH), scale / shift from the LDS tables
@@ -161,8 +175,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   constexpr bool kLift = KG < 8;
   const int beg = kLift ? 0 : a.ptr[so], end = kLift ? 1 : a.ptr[so + 1];
   const int2* __restrict__ idx = a.idx;
-  const float4* __restrict__ W4 = (const float4*)a.blocks;
-  const float4* xw = (const float4*)a.X + (size_t)rt * a.S_in * 512 + lane;
+  // buffer resources: this wave's row tile of the activations (all its input
+  // slabs; S_in = 0 is the microbenchmark's every-tile-reads-tile-0 mode), the
+  // packed weight blocks
+  const int rt_u = __builtin_amdgcn_readfirstlane(rt);
+  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const char*)a.X + (size_t)rt_u * a.S_in * 8192), 0, (a.S_in ? a.S_in : a.n_out_slabs) * 8192, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wres =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.blocks, 0, a.n_blocks * 16384, 0x00020000);
+  const int xlo = lane * 16, wlo = threadIdx.x * 16;
   const float al = a.alpha;
   const float* tsc = nullptr;
   const float* tsh = nullptr;
@@ -177,7 +198,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   const int tbase = (rt * S_out + so) * 512 + lane;
   DECLX(xa)
   DECLX(xb)
-  int2 ia = kLift ? make_int2(0, so) : idx[beg], ib = ia;
+  // list entries are wave-uniform: kept in scalar registers
+#define UIDX(E) ({ const int2 t_ = idx[(E)]; make_int2(__builtin_amdgcn_readfirstlane(t_.x), __builtin_amdgcn_readfirstlane(t_.y)); })
+  int2 ia = kLift ? make_int2(0, so) : UIDX(beg), ib = ia;
   LOADW(ia.y, 0)
   LOADX(xa, ia.x)
   // accumulators start at bias + residual (the MFMAs add onto them)
@@ -229,7 +252,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   for (int e = beg; e < end; e += 2) {
     const bool n1 = e + 1 < end;
     if (n1) {
-      ib = idx[e + 1];
+      ib = UIDX(e + 1);
       LOADW(ib.y, 1)
       LOADX(xb, ib.x)
     }
@@ -238,7 +261,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
     if (n1) {
       const bool n2 = e + 2 < end;
       if (n2) {
-        ia = idx[e + 2];
+        ia = UIDX(e + 2);
         LOADW(ia.y, 0)
         LOADX(xa, ia.x)
       }
@@ -465,6 +488,7 @@ void launch_gemm_bs(const GemmArgs& a, hipStream_t s) {
   }
 #undef LAUNCH
 #undef LAUNCHK
+#undef UIDX
 }
 
 }  // namespace lcn

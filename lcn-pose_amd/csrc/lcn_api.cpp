@@ -711,6 +711,7 @@ int gemm(Handle* h, const GemmCall& c, int B) {
   a.order = c.order;
   a.tail = tail_groups();
   a.k_groups = c.k_groups;
+  a.n_blocks = (c.ptr == h->fwd_ptr || c.ptr == h->bwd_ptr) ? h->nblk : h->nslab;  // hidden / thin layer
   a.bias = c.bias;
   a.pro_mode = c.X.mode;
   if (c.X.mode == PRO_BNACT) {

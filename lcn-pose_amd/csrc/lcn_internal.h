@@ -112,6 +112,7 @@ struct GemmArgs {
   const int* order;                  // output slabs by falling list length (tail schedule), or null
   int tail;                          // row-tile groups per XCD scheduled longest-list-first at the end
   int k_groups;                      // 8-feature groups of an input slab that are non-zero (5 / 7: the lift), 0 = all 8
+  int n_blocks;                      // 64x64 blocks in `blocks` (bounds of the weight loads)
   const float* bias;                 // [n_out_slabs*64] or null
   int pro_mode;                      // PRO_RAW or PRO_BNACT
   const float* pro_scale;            // forward BN scale / shift of the input's layer [F]
