@@ -41,9 +41,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int chunk = wg / a.ngroups, gi = wg - chunk * a.ngroups;
   const int4 grp = a.groups[gi];
-  const int so = grp.x, b0 = grp.y, b1 = grp.z;
+  // workgroup-uniform: kept in scalar registers (they form the scalar offsets of the operand loads)
+  const int so = __builtin_amdgcn_readfirstlane(grp.x), b0 = __builtin_amdgcn_readfirstlane(grp.y),
+            b1 = __builtin_amdgcn_readfirstlane(grp.z);
   const bool two = b1 >= 0;
-  const int si0 = a.blk[b0].x, si1 = two ? a.blk[b1].x : si0;
+  const int si0 = __builtin_amdgcn_readfirstlane(a.blk[b0].x);
+  const int si1 = two ? __builtin_amdgcn_readfirstlane(a.blk[b1].x) : si0;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int lr = lane & 31, h = lane >> 5;
   const int bi = w >> 1, hp = w & 1;
@@ -74,9 +77,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   // rows, sr and sr + 16, of the stage's row tile (float4 c40, c40 + 16 of the
   // slab: chunk g = t >> 5, lane half (t >> 4) & 1) -- one set of channel
   // constants serves both
-  const float4* A4 = (const float4*)a.A;
-  const float4* D4 = (const float4*)a.D;
-  const float4* Z4 = (const float4*)a.d_z;
   const int S_a = a.S_a, S_d = a.S_d;
   const int sr = t & 15;
   const int c40 = (t >> 5) * 64 + ((t >> 4) & 1) * 32 + sr, c41 = c40 + 16;
@@ -85,23 +85,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
 #define DW_IX(RT, S, SL, C4) (((size_t)(RT) * (S) + (SL)) * 512 + (C4))
 #ifdef EXP_DW_HOT  // diagnostic build: every stage reads one of four row tiles (operands stay in L2)
 #define DW_TILE(BASE) (((BASE) / kRT) & 3)
+  const int tile0 = 0;
 #else
 #define DW_TILE(BASE) ((BASE) / kRT)
+  const int tile0 = r0 / kRT;
 #endif
+  // Operand loads are buffer loads (gemm_bs.hip): one resource per operand over
+  // this chunk's row tiles, the (tile, slab) part of the address in scalar
+  // registers, this thread's two float4 slots as constant lane offsets.
+#ifdef EXP_DW_HOT
+  const int ntile = 4;
+#else
+  const int ntile = max(0, (r1 - r0 + kRT - 1) / kRT);
+#endif
+  const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const char*)a.A + (size_t)tile0 * S_a * 8192), 0, ntile * S_a * 8192, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const char*)a.D + (size_t)tile0 * S_d * 8192), 0, ntile * S_d * 8192, 0x00020000);
+  const __amdgpu_buffer_rsrc_t zres = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const char*)(DBB ? a.d_z : a.D) + (size_t)tile0 * S_d * 8192), 0, ntile * S_d * 8192, 0x00020000);
+  typedef float v4f_t __attribute__((ext_vector_type(4)));
+#define DW_BUFLD(RES, VOFF, SOFF)                                                      \
+  ({                                                                                   \
+    const v4f_t v_ = __builtin_bit_cast(v4f_t, __builtin_amdgcn_raw_buffer_load_b128((RES), (VOFF), (SOFF), 0)); \
+    make_float4(v_.x, v_.y, v_.z, v_.w);                                               \
+  })
+  const int v40 = c40 * 16, v41 = c41 * 16;
 #define DW_GLOAD(BASE)                                                     \
   {                                                                        \
-    const int t_ = DW_TILE(BASE);                                          \
-    ra0 = A4[DW_IX(t_, S_a, si0, c40)];                                    \
-    ra1 = A4[DW_IX(t_, S_a, si0, c41)];                                    \
+    const int t_ = DW_TILE(BASE) - tile0;                                  \
+    const int oa0 = (t_ * S_a + si0) * 8192, od = (t_ * S_d + so) * 8192;  \
+    ra0 = DW_BUFLD(ares, v40, oa0);                                        \
+    ra1 = DW_BUFLD(ares, v41, oa0);                                        \
     if (two) {                                                             \
-      rb0 = A4[DW_IX(t_, S_a, si1, c40)];                                  \
-      rb1 = A4[DW_IX(t_, S_a, si1, c41)];                                  \
+      const int oa1 = (t_ * S_a + si1) * 8192;                             \
+      rb0 = DW_BUFLD(ares, v40, oa1);                                      \
+      rb1 = DW_BUFLD(ares, v41, oa1);                                      \
     }                                                                      \
-    rd0 = D4[DW_IX(t_, S_d, so, c40)];                                     \
-    rd1 = D4[DW_IX(t_, S_d, so, c41)];                                     \
+    rd0 = DW_BUFLD(dres, v40, od);                                         \
+    rd1 = DW_BUFLD(dres, v41, od);                                         \
     if constexpr (DBB) {                                                   \
-      rz0 = Z4[DW_IX(t_, S_d, so, c40)];                                   \
-      rz1 = Z4[DW_IX(t_, S_d, so, c41)];                                   \
+      rz0 = DW_BUFLD(zres, v40, od);                                       \
+      rz1 = DW_BUFLD(zres, v41, od);                                       \
     }                                                                      \
   }
   if (r0 < r1) DW_GLOAD(r0);
@@ -202,6 +227,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
     __builtin_amdgcn_s_setprio(0);
   }
 #undef DW_GLOAD
+#undef DW_BUFLD
 #undef DW_TILE
 #undef DW_IX
   if (two) {
