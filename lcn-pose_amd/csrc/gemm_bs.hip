@@ -61,6 +61,7 @@ namespace lcn {
 // slab loop's 12 loads per 64 MFMAs 83.7 % of the MFMA peak as global loads,
 // 88.4 % as buffer loads, all L2 hits); reads past a resource return 0.
 typedef float v4f_t __attribute__((ext_vector_type(4)));
+typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
 #define BUFLD(RES, VOFF, SOFF)                                                         \
   ({                                                                                   \
     const v4f_t v_ = __builtin_bit_cast(v4f_t, __builtin_amdgcn_raw_buffer_load_b128((RES), (VOFF), (SOFF), 0)); \
@@ -81,10 +82,10 @@ typedef float v4f_t __attribute__((ext_vector_type(4)));
 // LDS-DMA (buffer_load_dwordx4 ... lds: no VGPRs, no ds_write; each wave
 // instruction lands 1 KB lane-linear, which is the fragment-packed order)
 #define GLDS(SOFF, DST) \
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(wres, (__attribute__((address_space(3))) void*)(DST), 16, wlo, (SOFF), 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(wres, (__attribute__((address_space(3))) void*)(DST), 16, xlo, (SOFF), 0, 0);
 #define LOADW(BLK, BUF)                                                   \
   {                                                                       \
-    const int bo_ = (BLK) * 16384;                                        \
+    const int bo_ = (BLK) * 16384 + wv_u * 1024;  /* this wave's 1 KB of each 4 KB quarter */ \
     float4* d_ = Wl + (BUF) * 1024 + (threadIdx.x & ~63);                 \
     GLDS(bo_, d_) GLDS(bo_ + 4096, d_ + 256) GLDS(bo_ + 8192, d_ + 512)   \
     if constexpr (KG > 6) GLDS(bo_ + 12288, d_ + 768)                     \
@@ -167,7 +168,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
     rtg = g0 + (R - T) + (j - rank * T);
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
-  const int rt_raw = rtg * kGemmWaves + w;
+  // the wave index and everything derived from it are wave-uniform: scalar registers
+  const int wv_u = __builtin_amdgcn_readfirstlane(w);
+  const int rt_raw = rtg * kGemmWaves + wv_u;
   const bool live = rt_raw < a.n_rt;
   // waves past the last row tile recompute it (they take part in the barriers)
   const int rt = live ? rt_raw : a.n_rt - 1;
@@ -178,12 +181,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   // buffer resources: this wave's row tile of the activations (all its input
   // slabs; S_in = 0 is the microbenchmark's every-tile-reads-tile-0 mode), the
   // packed weight blocks
-  const int rt_u = __builtin_amdgcn_readfirstlane(rt);
+  const int rt_u = rt;
   const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
       (void*)((const char*)a.X + (size_t)rt_u * a.S_in * 8192), 0, (a.S_in ? a.S_in : a.n_out_slabs) * 8192, 0x00020000);
   const __amdgpu_buffer_rsrc_t wres =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.blocks, 0, a.n_blocks * 16384, 0x00020000);
-  const int xlo = lane * 16, wlo = threadIdx.x * 16;
+  const int xlo = lane * 16;  // the one address register of every operand load
+  // this wave's row tile of a buffer in the output's layout (Y, residual source, z of the layer below)
+#define OUT_RES(PTR) \
+  __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)(PTR) + (size_t)rt * S_out * 8192), 0, S_out * 8192, 0x00020000)
   const float al = a.alpha;
   const float* tsc = nullptr;
   const float* tsh = nullptr;
@@ -194,8 +200,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   // bias / residual / table loads below are batched behind them, so the
   // prologue waits for memory once (not once per accumulator quarter)
   const int S_out = a.S_out, ncols = S_out * kSlab;
-  // float4 index of chunk 0 (fits 32 bits: max_batch * 17F <= INT32_MAX is checked at create)
-  const int tbase = (rt * S_out + so) * 512 + lane;
   DECLX(xa)
   DECLX(xb)
   // list entries are wave-uniform: kept in scalar registers
@@ -215,7 +219,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   }
   if (a.addsrc) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) rq[q] = ((const float4*)a.addsrc)[tbase + q * 64];
+    for (int q = 0; q < 8; ++q) rq[q] = BUFLD(OUT_RES(a.addsrc), xlo + (q & 3) * 1024, so * 8192 + (q >> 2) * 4096);
   } else {
 #pragma unroll
     for (int q = 0; q < 8; ++q) rq[q] = zero4;
@@ -271,30 +275,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   }
 
   // ---- epilogue ----
-  // The tile index is rebuilt here instead of being carried through the loop
-  // (as a 64-bit address offset it cost the BN-apply instance two spilled
-  // registers); the empty asm keeps the compiler from reusing the earlier value.
-  int rt_e = rt;
-  asm volatile("" : "+v"(rt_e));
-  const int tbase_e = (rt_e * S_out + so) * 512 + lane;
   if constexpr (EPI == EPI_BNBACK || EPI == kEpiBnBackDrop) {
     // z of the layer below, issued before the output stores so its latency
     // overlaps them (keeping it live through the loop would cost 32 VGPRs,
     // i.e. a wave per SIMD of occupancy)
-    const float4* Z4 = (const float4*)a.epi_z + tbase_e;
-    zp0 = Z4[0]; zp1 = Z4[64]; zp2 = Z4[128]; zp3 = Z4[192];
-    zp4 = Z4[256]; zp5 = Z4[320]; zp6 = Z4[384]; zp7 = Z4[448];
+    const __amdgpu_buffer_rsrc_t zres = OUT_RES(a.epi_z);
+    const int zo = so * 8192;
+    zp0 = BUFLD(zres, xlo, zo);        zp1 = BUFLD(zres, xlo + 1024, zo);
+    zp2 = BUFLD(zres, xlo + 2048, zo); zp3 = BUFLD(zres, xlo + 3072, zo);
+    zp4 = BUFLD(zres, xlo, zo + 4096);        zp5 = BUFLD(zres, xlo + 1024, zo + 4096);
+    zp6 = BUFLD(zres, xlo + 2048, zo + 4096); zp7 = BUFLD(zres, xlo + 3072, zo + 4096);
   }
   float v[32];
 #pragma unroll
   for (int k = 0; k < 16; ++k) { v[k] = acc0[k]; v[16 + k] = acc1[k]; }
   if (live) {
-    float4* Y = (float4*)a.Y;
+    const __amdgpu_buffer_rsrc_t yres = OUT_RES(a.Y);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      Y[tbase_e + q * 64] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-      Y[tbase_e + (4 + q) * 64] =
-          make_float4(v[16 + 4 * q], v[16 + 4 * q + 1], v[16 + 4 * q + 2], v[16 + 4 * q + 3]);
+    for (int q = 0; q < 8; ++q) {
+      const v4f_t o_ = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};  // chunk q: features 8q + 4h .. +3
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_t, o_), yres, xlo + (q & 3) * 1024,
+                                             so * 8192 + (q >> 2) * 4096, 0);
     }
   }
 #ifdef EXP_CLOCK
@@ -489,6 +490,7 @@ void launch_gemm_bs(const GemmArgs& a, hipStream_t s) {
 #undef LAUNCH
 #undef LAUNCHK
 #undef UIDX
+#undef OUT_RES
 }
 
 }  // namespace lcn

@@ -42,8 +42,19 @@ __global__ __launch_bounds__(256, 2) void gemm_bs_small_kernel(GemmArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
   const int beg = a.ptr[so], end = a.ptr[so + 1];
   const int2* __restrict__ idx = a.idx;
-  const float4* __restrict__ W4 = (const float4*)a.blocks + lane;
-  const float4* __restrict__ xw = (const float4*)a.X + (size_t)rt * a.S_in * 512 + lane;
+  // operand loads are buffer loads (see gemm_bs.hip): this row tile of the
+  // activations and the packed weight blocks as scalar resources, one 32-bit
+  // offset register per lane, the slab / block part of the address scalar
+  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const char*)a.X + (size_t)rt * a.S_in * 8192), 0, a.S_in * 8192, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wres =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.blocks, 0, a.n_blocks * 16384, 0x00020000);
+  const int xlo = lane * 16;
+  typedef float v4f_t __attribute__((ext_vector_type(4)));
+  auto bufld = [&](const __amdgpu_buffer_rsrc_t& r, int voff, int soff) {
+    const v4f_t v = __builtin_bit_cast(v4f_t, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+    return make_float4(v.x, v.y, v.z, v.w);
+  };
   const float al = a.alpha;
   const int spj = a.spj_in;
 
@@ -61,14 +72,13 @@ __global__ __launch_bounds__(256, 2) void gemm_bs_small_kernel(GemmArgs a) {
   if constexpr (PRO == PRO_BNACT || EPI == EPI_BNBACK) __syncthreads();
 
   auto load = [&](SlabRegs& s, int e) {
-    const int2 ix = idx[e];
-    const float4* xs = xw + (size_t)ix.x * 512;
-    const float4* ws = W4 + (size_t)ix.y * 1024;
+    const int2 ix = idx[e];  // wave-uniform
+    const int si = __builtin_amdgcn_readfirstlane(ix.x), blk = __builtin_amdgcn_readfirstlane(ix.y);
 #pragma unroll
-    for (int g = 0; g < 8; ++g) s.x[g] = xs[g * 64];
+    for (int g = 0; g < 8; ++g) s.x[g] = bufld(xres, xlo + (g & 3) * 1024, si * 8192 + (g >> 2) * 4096);
 #pragma unroll
-    for (int g = 0; g < 16; ++g) s.w[g] = ws[g * 64];
-    return ix.x;
+    for (int g = 0; g < 16; ++g) s.w[g] = bufld(wres, xlo + (g & 3) * 1024, blk * 16384 + (g >> 2) * 4096);
+    return si;
   };
   f32x16 acc0, acc1;
 #pragma unroll
