@@ -254,11 +254,11 @@ int dw_chunks(int nblk, int64_t B) {
 
 // Launches of at most this many 32-row tiles run the small-batch kernel, which
 // splits every slab list over the four waves of a workgroup: measured faster
-// up to batch 2048 (0.92 -> 0.59 ms per step at batch 200, 1.24 -> 1.01 ms at
-// 1024, 1.48 -> 1.43 ms at 2048), slower from 2560 on (1.56 -> 1.57 ms; 4096:
-// 1.91 -> 2.11 ms).  LCN_SMALL_RT overrides, 0 = never.
+// up to batch 2560 (0.92 -> 0.57 ms per step at batch 200, 1.24 -> 0.89 ms at
+// 1024, 1.40 -> 1.29 ms at 2048, 1.49 -> 1.44 ms at 2560), slower from 3072 on
+// (1.56 -> 1.61 ms).  LCN_SMALL_RT overrides, 0 = never.
 int small_row_tiles() {  // read when a handle is created
-  return std::getenv("LCN_SMALL_RT") ? std::atoi(std::getenv("LCN_SMALL_RT")) : 72;
+  return std::getenv("LCN_SMALL_RT") ? std::atoi(std::getenv("LCN_SMALL_RT")) : 80;
 }
 
 // ---------------------------------------------------------------------------

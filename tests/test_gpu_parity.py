@@ -25,15 +25,15 @@ CASES = [
     ("lc_nobn", dict(F=64, L=1, knn=2, batch_norm=False), 128),
     ("lc_noclip_reg", dict(F=64, L=1, knn=2, max_norm=False, regularization=0.01), 64),
     ("lc_tiny_B7", dict(F=64, L=1, knn=3), 7),
-    # 72 row tiles: the largest batch of the small-batch GEMM; 73: the first of the other
-    ("lc_B2304", dict(F=64, L=1, knn=2), 2304),
-    ("lc_B2310", dict(F=64, L=1, knn=2), 2310),
+    # 80 row tiles: the largest batch of the small-batch GEMM; 81: the first of the other
+    ("lc_B2560", dict(F=64, L=1, knn=2), 2560),
+    ("lc_B2570", dict(F=64, L=1, knn=2), 2570),
     # BASELINE.json configs[4] (cfg5) model shape: knn 5, 3 blocks
     ("cfg5_knn5_L3", dict(F=64, L=3, knn=5), 512),
 ]
 
 
-# Batches of up to 2304 rows run the small-batch GEMM kernel (gemm_small.hip);
+# Batches of up to 2560 rows run the small-batch GEMM kernel (gemm_small.hip);
 # LCN_SMALL_RT=0 at handle creation keeps such a batch on the large-batch
 # kernel (gemm_bs.hip), so both are held to the oracle on the same cases.
 @pytest.fixture(params=["small_batch_gemm", "large_batch_gemm"])
