@@ -38,8 +38,8 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 #define GLDS(SRC, DST) \
   __builtin_amdgcn_global_load_lds((const void*)(SRC), (__attribute__((address_space(3))) void*)(DST), 16, 0, 0);
 
-template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void loop_kernel(
+template <int MODE, int WPE = 4>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void loop_kernel(
     int iters, const float4* __restrict__ X, const float4* __restrict__ W, int n_tiles, float* out) {
   extern __shared__ __attribute__((aligned(16))) float4 Wl[];  // [2][1024]
   __shared__ __attribute__((aligned(16))) float4 Wa[(MODE == 5 || MODE == 6) ? 1024 : 1];
@@ -140,15 +140,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
-template <int MODE>
+template <int MODE, int WPE = 4>
 static void run(int iters, const float4* X, const float4* W, int n_tiles, float* out, int grid) {
+  grid = grid / 4 * WPE;
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   float best = 1e30f;
   for (int rep = 0; rep < 3; ++rep) {
     (void)hipEventRecord(e0, 0);
-    hipLaunchKernelGGL(loop_kernel<MODE>, dim3(grid), dim3(256), 2 * 1024 * sizeof(float4), 0, iters, X, W, n_tiles, out);
+    hipLaunchKernelGGL((loop_kernel<MODE, WPE>), dim3(grid), dim3(256), 2 * 1024 * sizeof(float4), 0, iters, X, W, n_tiles, out);
     (void)hipEventRecord(e1, 0);
     if (hipEventSynchronize(e1) != hipSuccess) { std::printf("mode %d failed\n", MODE); return; }
     float ms;
@@ -156,7 +157,7 @@ static void run(int iters, const float4* X, const float4* W, int n_tiles, float*
     best = ms < best ? ms : best;
   }
   const double flop = (double)grid * 4 * iters * 64 * 4096.0;
-  std::printf("mode %d: %.2f ms, %.1f TFLOP/s (%.1f%% of 157.3)\n", MODE, best, flop / (best * 1e-3) / 1e12,
+  std::printf("mode %d (%d workgroups per CU): %.2f ms, %.1f TFLOP/s (%.1f%% of 157.3)\n", MODE, WPE, best, flop / (best * 1e-3) / 1e12,
               100.0 * flop / (best * 1e-3) / 1e12 / 157.3);
 }
 
@@ -182,5 +183,9 @@ int main(int argc, char** argv) {
   run<6>(iters, X, W, n_tiles, out, grid);
   run<7>(iters, X, W, n_tiles, out, grid);
   run<8>(iters, X, W, n_tiles, out, grid);
+  run<7, 3>(iters, X, W, n_tiles, out, grid);
+  run<8, 3>(iters, X, W, n_tiles, out, grid);
+  run<7, 2>(iters, X, W, n_tiles, out, grid);
+  run<8, 2>(iters, X, W, n_tiles, out, grid);
   return 0;
 }
