@@ -397,7 +397,7 @@ def main(argv=None):
                 "avg_launch_ms": round(d["avg_ms"], 4)}
         # the metric's "achieved HBM GB/s vs peak", for the hidden-layer forward
         # GEMM (the north star's fused LCN forward): algorithmic bytes = read the
-        # input activations + write z, 2 x 17*F floats per pose (SURVEY §8d)
+        # input activations + write z, 2 x 17*F floats per pose
         hbm_ew = None
         nba, msba, bytes_ba = bn_act_timing
         if nba:
@@ -441,7 +441,7 @@ def main(argv=None):
                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr,
                    "traffic_GBps": round(tr / (f["avg_ms"] * 1e-3) / 1e9, 1) if tr else None,
                    "mfma_frac": round(f["tflops"] / FP32_PEAK_TFLOPS, 4),
-                   "note": "compute-bound: 165 FLOP/B vs a 19.7 FLOP/B fp32 ridge (DESIGN.md)"}
+                   "note": "compute-bound: 165 FLOP/B vs a 19.7 FLOP/B fp32 ridge (157.3 TFLOP/s over 8 TB/s)"}
         res = {
             "metric": METRIC, "value": round(value, 1), "unit": "poses/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),

@@ -121,7 +121,7 @@ int lcn_device_buffer(void* handle, int32_t slot, int64_t bytes, void** dptr);
 int lcn_memcpy_h2d(void* handle, void* dst, const void* src, int64_t bytes);
 int lcn_memcpy_d2h(void* handle, void* dst, const void* src, int64_t bytes);
 
-/* --- device-resident datasets --------------------- */
+/* --- device-resident datasets ------------------------------------------- */
 /* The reference feeds every step from host numpy arrays: fit() fancy-indexes
  * the float64 train arrays with a permutation deque (models_att.py:193-212),
  * predict() slices fixed zero-padded batches (:88-121), inference.py
@@ -201,7 +201,7 @@ int lcn_comm_init_host(void* handle, int32_t rank, int32_t world, lcn_host_allre
 int lcn_comm_suspend(void* handle, int32_t suspend);
 int lcn_comm_allreduce_host(void* handle, double* values, int32_t count, int32_t op /* 0 sum, 1 max */);
 
-/* --- evaluation -------------------------------------- */
+/* --- evaluation --------------------------------------------------------- */
 /* evaluate.py's per-frame loop (evaluate.py:53-73) in one launch, float64:
  * every frame's prediction goes from the image frame to the camera frame
  * (tools/tools.py:183-194: box width / 2000 depth ratio, root depth, pinhole

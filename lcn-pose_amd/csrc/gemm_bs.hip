@@ -29,7 +29,7 @@
 // start held 32 VGPRs through the loop and cost a wave per SIMD: 4 waves/SIMD
 // at <= 128 VGPRs is 3 % faster for the dX GEMM).  Measured
 // against a 128x64 LDS-staged tile with two barriers per slab: 124 vs 114
-// TFLOP/s at cfg3.
+// TFLOP/s at B = 65 536, knn 3.
 //
 // Operand prologue (PRO):  PRO_RAW a = X;  PRO_BNACT a = leaky(scale X + shift)
 // (BN apply + LeakyReLU of the input's layer, scale/shift tables in LDS).

@@ -24,7 +24,7 @@ __device__ __forceinline__ float4 bnact4(float4 v, float4 sc, float4 sh, float a
   return v;
 }
 
-// BN + LeakyReLU backward (SURVEY Appendix A):
+// BN + LeakyReLU backward:
 //   u = scale*z + shift,  du = u > 0 ? dh : alpha*dh,  dz = c1*du + c2 + c3*z
 struct BnBackCoef { float4 sc, sh, c1, c2, c3; };
 

@@ -1,5 +1,5 @@
 // Device-resident datasets: permutation gather, test-time augmentation and
-// its undo (gfx950).  SURVEY §8(f) rows 2 and 3.
+// its undo (gfx950).
 //
 // The reference feeds every step from the host: fit() draws batch indices
 // from a deque of np.random.permutation()s and fancy-indexes the float64

@@ -160,7 +160,7 @@ void launch_bn_fwd_finalize(const double2* col, const TilePartials& tp, int H, i
                      F, phase, rows, ri, gamma, beta, eps, acc, st, zsum);
 }
 
-// Backward BN finish per channel (SURVEY Appendix A):  dz = c1*du + c2 + c3*z,
+// Backward BN finish per channel:  dz = c1*du + c2 + c3*z,
 //   c1 = gamma*rstd, c3 = -c1*rstd*S2/N, c2 = -c1*S1/N - c3*mean,
 //   S1 = sum du = dbeta, S2 = sum du*zhat = dgamma.
 // The bias gradient of the layer is sum_b dz per column:

@@ -1,5 +1,4 @@
-// Batched MPJPE / P-MPJPE of evaluate.py on the device (gfx950), SURVEY §8(f)
-// row 4.
+// Batched MPJPE / P-MPJPE of evaluate.py on the device (gfx950).
 //
 // The reference evaluates one frame at a time in a Python loop
 // (evaluate.py:53-73): image_to_camera_frame (tools/tools.py:183-194), for

@@ -260,7 +260,7 @@ void launch_maskgrad(const double* blocksum, int nl, const float* M, const float
 }
 
 // Fused gradient finish + Adam over the flat parameter vector.  Weights get
-// the clip/mask backward  g = dWe * M[i,j] / n - c_l * W  (SURVEY App. A).
+// the clip/mask backward  g = dWe * M[i,j] / n - c_l * W .
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ theta, float* __restrict__ m,
                                                    float* __restrict__ v,
                                                    const float* __restrict__ rg,

@@ -1268,7 +1268,7 @@ int lcn_train_step(void* handle, const float* x, const float* labels, int64_t B,
 }
 
 // ---------------------------------------------------------------------------
-// device-resident datasets (SURVEY §8f rows 2-3)
+// device-resident datasets
 // ---------------------------------------------------------------------------
 static int dataset_of(Handle* h, int32_t slot, Handle::Dataset** d) {
   if (slot < 0 || slot >= (int)h->datasets.size() || !h->datasets[slot].ptr) {

@@ -23,8 +23,8 @@ variable names the reference graph gives its variables (``tf_name_map``):
 Keras BN moving statistics are written as their initial values (0, 1): the
 reference never runs their update ops (it trains and predicts with batch
 statistics, models_att.py:588-612).  These names follow TF1 / Keras naming
-rules; they are unverified against a real TF checkpoint (none exists offline,
-SURVEY §8f).  ``restore`` reads these files, and the earlier ``.npz`` payload.
+rules; they are unverified against a real TF checkpoint (none exists offline).
+``restore`` reads these files, and the earlier ``.npz`` payload.
 """
 from __future__ import annotations
 

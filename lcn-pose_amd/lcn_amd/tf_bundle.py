@@ -19,7 +19,7 @@ The reference saves with ``tf.compat.v1.train.Saver`` (models_att.py:161-162,
 Protobuf messages are encoded / decoded by hand (a handful of varint and
 length-delimited fields).  CRC-32C comes from liblcn (lcn_crc32c).  Parity
 with real TensorFlow files is unpinned: TensorFlow is not installed here and
-the reference ships no checkpoint (SURVEY §8f); the format follows the public
+the reference ships no checkpoint; the format follows the public
 specification above and is checked by round trips, known-answer CRCs and a
 strict reader.
 """

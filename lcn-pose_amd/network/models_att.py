@@ -6,7 +6,7 @@ experiment/<dir_name>/{checkpoints/{final,best},summaries} layout (:431-433).
 The TensorFlow graph + Session is replaced by liblcn.so (HIP kernels for
 gfx950) through lcn_amd.native; there is no CPU compute path.
 
-Deliberate differences from the reference, all documented in DESIGN.md:
+Deliberate differences from the reference:
   * dropout masks come from liblcn's counter-based generator (TF's random
     stream cannot be reproduced); rate, scaling and placement are TF's;
   * resuming from a checkpoint restores the weights AND keeps them (the

@@ -362,7 +362,7 @@ def reg_loss(cfg: Config, params, dtype=np.float64) -> float:
 
 
 # ----------------------------------------------------------------------------
-# Backward (analytic; SURVEY Appendix A)
+# Backward (analytic)
 # ----------------------------------------------------------------------------
 
 def _bn_act_backward(cfg, dh, rec, F, gamma, pos=None):

@@ -42,7 +42,7 @@ def perturbed_params(cfg, seed=1):
 
 
 def synthetic_batch(B, in_F=2, seed=0):
-    """x ~ U(-1,1) [B, 17*in_F]; labels = lifted x + noise (SURVEY §8d)."""
+    """x ~ U(-1,1) [B, 17*in_F]; labels = lifted x + noise."""
     rng = np.random.default_rng(seed)
     x = rng.uniform(-1, 1, size=(B, 17 * in_F)).astype(np.float32)
     x3 = x.reshape(B, 17, in_F)

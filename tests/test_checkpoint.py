@@ -1,4 +1,4 @@
-"""TensorFlow tensor-bundle checkpoint I/O (SURVEY §8f row 1), CPU only.
+"""TensorFlow tensor-bundle checkpoint I/O, CPU only.
 
 No TensorFlow and no reference checkpoint exist offline, so the format is
 pinned by published known answers (CRC-32C check values, the leveldb footer

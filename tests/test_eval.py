@@ -1,4 +1,4 @@
-"""Batched MPJPE / P-MPJPE (SURVEY §8f row 4): evaluate.py's per-frame loop
+"""Batched MPJPE / P-MPJPE: evaluate.py's per-frame loop
 (evaluate.py:53-73) as one device launch, lcn_eval_mpjpe.
 
 Bars: the oracle (oracle/eval_oracle.py) reproduces the reference's own

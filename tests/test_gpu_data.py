@@ -1,4 +1,4 @@
-"""Device-resident datasets on the MI355X (SURVEY §8f rows 2-3): permutation
+"""Device-resident datasets on the MI355X: permutation
 gather, fixed-batch predict with zero padding, test-time augmentation.
 
 Bars: the gathered batch is bit-identical to the reference's host path

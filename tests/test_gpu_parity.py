@@ -1,6 +1,6 @@
 """HIP path vs the CPU oracle (runs on the MI355X box: pytest -m gpu).
 
-Tolerances (north star "1e-4"): forward outputs |d| <= 1e-4 in
+Tolerances: forward outputs |d| <= 1e-4 in
 normalised units against the float64 oracle; gradients <= 1e-4 relative
 (per tensor, L2) against float64; one Adam step |d theta| <= 1e-6 absolute.
 """

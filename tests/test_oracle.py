@@ -28,7 +28,7 @@ def test_neighbour_matrix_matches_notebook_dumps(golden_dir):
 
 
 def test_block_counts():
-    # SURVEY §8(a): nnz 57/111/175/273 for knn 1/2/3/5
+    # nnz 57/111/175/273 for knn 1/2/3/5
     for knn, nnz in ((1, 57), (2, 111), (3, 175), (5, 273)):
         assert int(O.neighbour_matrix(knn).sum()) == nnz
 
