@@ -268,40 +268,6 @@ void launch_bn_act(const float* z, const float* res, float* h, const float* scal
                      (const float4*)res, (float4*)h, scale, shift, F, S, alpha, n4, drop);
 }
 
-// per-kEwRows-row column sums of a 1-slab row-tiled src (the output bias
-// gradient): lane = column, 4 waves split the rows
-__global__ __launch_bounds__(256) void colpart_kernel(const float* __restrict__ src, int B,
-                                                      int ncols, float2* __restrict__ part) {
-  __shared__ float red[4][64];
-  const int t = threadIdx.x, c = t & 63, w = t >> 6;
-  const int r0 = blockIdx.x * kEwRows, r1 = min(B, r0 + kEwRows);
-  float s = 0.f;
-  if (c < ncols)
-    for (int r = r0 + w; r < r1; r += 4) s += src[tix(r, c, 1)];
-  red[w][c] = s;
-  __syncthreads();
-  if (w == 0 && c < ncols)
-    part[(size_t)blockIdx.x * ncols + c] =
-        make_float2((red[0][c] + red[1][c]) + (red[2][c] + red[3][c]), 0.f);
-}
-
-void launch_colpart(const float* src, int B, int ncols, float2* part, hipStream_t s) {
-  hipLaunchKernelGGL(colpart_kernel, dim3((B + kEwRows - 1) / kEwRows), dim3(256), 0, s, src, B,
-                     ncols, part);
-}
-
-__global__ void col_to_float_kernel(const double2* __restrict__ col, int n, float* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  double x = 0.0;
-  for (int p = 0; p < kColSplit; ++p) x += col[(size_t)p * n + i].x;
-  out[i] = (float)x;
-}
-
-void launch_col_to_float(const double2* col, int n, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(col_to_float_kernel, dim3((n + 255) / 256), dim3(256), 0, s, col, n, out);
-}
-
 // The ranks' batch rows of a step: begin fills this rank's slot (the others
 // zero), an all-reduce (sum) gathers them, finish derives this rank's RowInfo.
 __global__ void rows_begin_kernel(double* rows, int world, int rank, double B) {

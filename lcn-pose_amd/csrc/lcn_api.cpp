@@ -111,10 +111,10 @@ struct Handle {
   float2* stat_part = nullptr;    // GEMM epilogue partials [tiles][H], tiles of stat_rows rows
   int stat_rows = kGemmRows;      // rows per partial of the last GEMM: 128, or 32 (small-batch kernel)
   int small_rt = 0;               // launches of at most this many row tiles use the small-batch GEMM
-  float2* col_part = nullptr;     // [B/kEwRows tiles][51] output-bias partials
   double2* colacc = nullptr;      // [kColSplit][H] float64 column sums
   float* dw_part = nullptr;
   double *loss_part = nullptr, *loss_sum = nullptr, *acc1 = nullptr, *acc2 = nullptr;
+  double* db_part = nullptr;      // [loss_grid][64] column sums of dy per out_assemble workgroup
   int loss_grid = 1;
 
   // Adam segments
@@ -523,10 +523,10 @@ int build(Handle* h, const lcn_config* c) {
   CHECK(dalloc(h, &h->c123, 3 * F));
   CHECK(dalloc(h, &h->stat_part,
                (size_t)std::max<int64_t>(cdiv(B, kGemmRows), std::min<int64_t>(cdiv(B, kRT), h->small_rt)) * H));
-  CHECK(dalloc(h, &h->col_part, (size_t)cdiv(B, kEwRows) * 64));
   CHECK(dalloc(h, &h->colacc, (size_t)kColSplit * H));
   h->loss_grid = (int)std::min<int64_t>(2048, cdiv(B, 4));
   CHECK(dalloc(h, &h->loss_part, (size_t)h->loss_grid));
+  CHECK(dalloc(h, &h->db_part, (size_t)h->loss_grid * 64));
   CHECK(dalloc(h, &h->loss_sum, 4));
   CHECK(dalloc(h, &h->acc1, 2 * F));
   CHECK(dalloc(h, &h->acc2, 2 * F));
@@ -900,17 +900,20 @@ int forward(Handle* h, int B, bool with_labels, bool train) {
   oa.out = h->out;
   oa.dy = train ? h->dy : nullptr;
   oa.loss_part = with_labels ? h->loss_part : nullptr;
+  // a training step: the output bias gradient db4 = sum_b dy comes out of the same pass
+  const bool want_db = train && with_labels;
+  oa.db_part = want_db ? h->db_part : nullptr;
   oa.rows = (double)B;
   oa.ri = rinfo(h);
   oa.B = B;
   const int ogrid = (int)std::min<int64_t>(h->loss_grid, cdiv(B, 4));
   launch_out_assemble(oa, ogrid, s);
-  if (with_labels) launch_loss_finalize(h->loss_part, ogrid, h->loss_sum, s);
+  if (with_labels)
+    launch_loss_finalize(h->loss_part, ogrid, h->loss_sum, oa.db_part, h->rg + h->b_off[nl - 1], s);
   return LCN_OK;
 }
 
 int backward(Handle* h, int B) {
-  hipStream_t s = h->stream;
   const int nl = h->nl, L = h->L;
   const int H = h->H, S = h->nslab;
   const WLayer& Lo = h->wl[nl - 1];
@@ -924,10 +927,7 @@ int backward(Handle* h, int B) {
                          h->DH, S, nullptr, EPI_BNBACK, top, -1, 0.0}, B));
   CHECK(gemm_dw(h, raw(h->Hb[L], S), raw(h->dy, 1), h->out_blk, S, h->rg + Lo.w_off, 51,
                 H, 51, B, LCN_K_OUT_DW));
-  const int ct = (int)cdiv(B, kEwRows);
-  launch_colpart(h->dy, B, 51, h->col_part, s);
-  launch_colreduce(h->col_part, ct, kEwRows, B, 51, 0, h->colacc, s);
-  launch_col_to_float(h->colacc, 51, h->rg + h->b_off[nl - 1], s);
+  // (db4 = sum_b dy was reduced with the loss, by out_assemble / loss_finalize)
 
   for (int l = L - 1; l >= 0; --l) {
     const int k1 = 2 * l + 1, k2 = 2 * l + 2;

@@ -13,7 +13,6 @@ constexpr int kSlab = 64;       // feature slab = MFMA tile edge; F is a multipl
 constexpr int kRT = 32;         // rows per row tile of the activation layout
 constexpr int kGemmWaves = 4;   // row tiles (one per wave) per block-sparse GEMM workgroup
 constexpr int kGemmRows = kRT * kGemmWaves;  // rows per workgroup = per BN partial
-constexpr int kEwRows = 256;    // rows per tile of the output-bias column partials
 
 // ----------------------------------------------------------------------------
 // Activation layout ("row tiles").  Every activation the step keeps in HBM --
@@ -178,6 +177,7 @@ struct OutAsmArgs {
   float* out;                        // [B][51] row-major
   float* dy;                         // 1-slab tiled, or null (padding written as 0)
   double* loss_part;                 // [gridDim] or null
+  double* db_part;                   // [gridDim][64] column sums of dy (the output bias gradient), or null
   double rows;                       // global batch rows: dy = 2 (out - lab) / (rows * 51)
   const RowInfo* ri;                 // several ranks: rows read from device memory
   int B;
@@ -258,12 +258,10 @@ void launch_bn_bwd_finalize(const double2* col, const TilePartials& tp, int H, i
 void launch_bn_act(const float* z, const float* res, float* h, const float* scale,
                    const float* shift, int F, float alpha, int B, int S, const Dropout& drop,
                    hipStream_t s);
-// per-kEwRows-tile column sums of a 1-slab tiled src (ncols <= 64 used) ->
-// part[tiles][ncols] as (sum, 0)
-void launch_colpart(const float* src, int B, int ncols, float2* part, hipStream_t s);
-// out[i] = (float) sum over the tile groups of col[.][i].x (col from colreduce with H = n)
-void launch_col_to_float(const double2* col, int n, float* out, hipStream_t s);
-void launch_loss_finalize(const double* part, int n, double* out, hipStream_t s);
+// sums the n workgroup partials of out_assemble: the loss, and (db_part given)
+// the 51 columns of dy into the output layer's bias gradient db_out
+void launch_loss_finalize(const double* part, int n, double* out, const double* db_part, float* db_out,
+                          hipStream_t s);
 
 // ----------------------------------------------------------------------------
 // Parameters: mask, clip_by_norm, masking, packing, gradients, Adam
