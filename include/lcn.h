@@ -175,7 +175,9 @@ int lcn_predict_dataset(void* handle, int32_t x_slot, int32_t lab_slot, int64_t 
  * size (world 1 included: the multi-GPU path then runs on one GPU) and may be
  * called once per handle (LCN_E_ARG otherwise).  After it, every step does
  * SyncBN (phased BN reductions + ncclAllReduce, float64) and one float32
- * all-reduce of the raw gradient vector on the handle's stream.
+ * all-reduce of the raw gradient vector on the handle's stream: 4L + 3
+ * collectives per training step with L blocks (the ranks' batch rows ride on
+ * BN layer 0's all-reduce, the loss sum on the first BN backward's).
  * lcn_comm_allreduce_host: count <= 2F doubles, a no-op without a
  * communicator. */
 int lcn_comm_unique_id(void* id_out /* 128 bytes */);
@@ -200,6 +202,13 @@ int lcn_comm_init_host(void* handle, int32_t rank, int32_t world, lcn_host_allre
  * exchanges while suspended. */
 int lcn_comm_suspend(void* handle, int32_t suspend);
 int lcn_comm_allreduce_host(void* handle, double* values, int32_t count, int32_t op /* 0 sum, 1 max */);
+/* What joins this handle to other ranks: kind LCN_COMM_*; rank / world as the
+ * communicator itself reports them (RCCL: ncclCommUserRank / ncclCommCount of
+ * the live communicator, so a caller can show that RCCL holds `world` ranks),
+ * 0 / 1 without one.  Any out pointer may be NULL.  No counterpart in the
+ * reference (single process, models_att.py:155). */
+enum { LCN_COMM_NONE = 0, LCN_COMM_RCCL = 1, LCN_COMM_HOST = 2 };
+int lcn_comm_info(void* handle, int32_t* kind, int32_t* rank, int32_t* world);
 
 /* --- evaluation --------------------------------------------------------- */
 /* evaluate.py's per-frame loop (evaluate.py:53-73) in one launch, float64:

@@ -153,9 +153,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   const int nso = a.n_out_slabs;
   const int n_rtg = (a.n_rt + kGemmWaves - 1) / kGemmWaves;
   const int xcd = blockIdx.x & 7, li = blockIdx.x >> 3;
-  const int per = (n_rtg + 7) >> 3;
-  const int g0 = xcd * per, R = min(per, n_rtg - g0);
-  if (R <= 0 || li >= R * nso) return;  // padding of the grid (uniform per workgroup)
+  // n_rtg = 8 base + extra: the first `extra` XCDs take one group more, so a
+  // batch that is not a multiple of 1024 rows still loads every XCD
+  const int base = n_rtg >> 3, extra = n_rtg & 7;
+  const int g0 = xcd * base + min(xcd, extra), R = base + (xcd < extra ? 1 : 0);
+  if (li >= R * nso) return;  // padding of the grid (uniform per workgroup)
   const int T = a.order ? min(R, a.tail) : 0;
   int rtg, so;
   if (li < (R - T) * nso) {

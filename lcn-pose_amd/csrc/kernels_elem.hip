@@ -118,14 +118,38 @@ __global__ __launch_bounds__(1024) void bn_fwd_finalize_kernel(
     ColSrc src, int H, int F, int phase, double rows,
     const RowInfo* __restrict__ ri, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, double* acc, BnStats st,
-    double* __restrict__ zsum) {
+    double* __restrict__ zsum, BnRider rider) {
   extern __shared__ double2 cs[];  // [H]
+  __shared__ double rows_sh;
   if (phase <= 1) {
     if (src.part) colsum_tiles_lds(src.part, src.n_tiles, src.tile_rows, src.B, H, 1, cs);
     else colsum_groups_lds(src.col, H, cs);
   }
   const int J = H / F;
-  const double count = (ri ? ri->rows_global : rows) * (double)J;
+  double rows_global = rows;
+  if (rider.kind == kRideRows) {
+    if (phase == 1) {  // this rank's slot of the one-hot row vector
+      for (int r = threadIdx.x; r < rider.world; r += blockDim.x)
+        acc[2 * F + r] = r == rider.rank ? rider.b_local : 0.0;
+    } else if (phase == 2) {  // every rank's rows -> this rank's RowInfo
+      if (threadIdx.x == 0) {
+        double total = 0.0, below = 0.0;
+        for (int r = 0; r < rider.world; ++r) {
+          const double v = acc[2 * F + r];
+          if (r < rider.rank) below += v;
+          total += v;
+        }
+        rider.ri_out->rows_global = total;
+        rider.ri_out->row0 = (int64_t)below;
+        rows_sh = total;
+      }
+      __syncthreads();
+      rows_global = rows_sh;
+    }
+  } else if (ri) {
+    rows_global = ri->rows_global;
+  }
+  const double count = rows_global * (double)J;
   for (int ch = threadIdx.x; ch < F; ch += blockDim.x) {
     double S = 0.0, Q = 0.0;
     if (phase <= 1) {
@@ -154,10 +178,11 @@ __global__ __launch_bounds__(1024) void bn_fwd_finalize_kernel(
 
 void launch_bn_fwd_finalize(const double2* col, const TilePartials& tp, int H, int F, int phase,
                             double rows, const RowInfo* ri, const float* gamma, const float* beta,
-                            float eps, double* acc, BnStats st, double* zsum, hipStream_t s) {
+                            float eps, double* acc, BnStats st, double* zsum, const BnRider& rider,
+                            hipStream_t s) {
   const ColSrc src{col, tp.part, tp.n_tiles, tp.tile_rows, tp.B};
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(1), dim3(1024), H * sizeof(double2), s, src, H,
-                     F, phase, rows, ri, gamma, beta, eps, acc, st, zsum);
+                     F, phase, rows, ri, gamma, beta, eps, acc, st, zsum, rider);
 }
 
 // Backward BN finish per channel:  dz = c1*du + c2 + c3*z,
@@ -173,8 +198,12 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
     const RowInfo* __restrict__ ri, double b_local, const float* __restrict__ gamma,
     const float* __restrict__ mean, const float* __restrict__ rstd, double* acc,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ c123,
-    const double* __restrict__ zsum, float* __restrict__ db) {
+    const double* __restrict__ zsum, float* __restrict__ db, BnRider rider) {
   extern __shared__ double2 cs[];  // [H]
+  if (rider.kind == kRideLoss && threadIdx.x == 0) {
+    if (phase == 1) acc[2 * F] = *rider.loss;
+    else if (phase == 2) *rider.loss = acc[2 * F];
+  }
   if (src.part) colsum_tiles_lds(src.part, src.n_tiles, src.tile_rows, src.B, H, 0, cs);
   else colsum_groups_lds(src.col, H, cs);
   const int J = H / F;
@@ -216,11 +245,11 @@ void launch_bn_bwd_finalize(const double2* col, const TilePartials& tp, int H, i
                             int bn, double rows, const RowInfo* ri, double b_local,
                             const float* gamma, const float* mean, const float* rstd, double* acc,
                             float* dgamma, float* dbeta, float* c123, const double* zsum, float* db,
-                            hipStream_t s) {
+                            const BnRider& rider, hipStream_t s) {
   const ColSrc src{col, tp.part, tp.n_tiles, tp.tile_rows, tp.B};
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(1024), H * sizeof(double2), s, src, H,
                      F, phase, bn, rows, ri, b_local, gamma, mean, rstd, acc, dgamma, dbeta, c123,
-                     zsum, db);
+                     zsum, db, rider);
 }
 
 // h = [res +] leaky(scale*z + shift) over row-tiled [B][S*64] buffers; the

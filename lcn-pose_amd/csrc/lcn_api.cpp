@@ -147,6 +147,7 @@ struct Handle {
   std::vector<char> host_stage;
   int rank = 0, world = 1;
   bool comm_off = false;          // lcn_comm_suspend: calls run rank-locally
+  bool loss_pending = false;      // the step's loss sum still has to be all-reduced (rides on the first BN backward)
   double* rows_all = nullptr;     // [world] the ranks' batch rows of the running step
   RowInfo* rowinfo = nullptr;     // global rows / first global row of this rank (device)
   // run the multi-GPU (phase 1 -> all-reduce -> phase 2) BN reductions without
@@ -157,6 +158,7 @@ struct Handle {
 
   // instrumentation
   int timing = 0;
+  std::string timer_err;  // first failure to create / record a timer event since lcn_set_timing
   // train-step graphs (world 1, no dropout, no timing): the device work of a
   // step captured once per (batch, update, keep_grads) and replayed -- small
   // batches are launch-bound (fit's reference batch is 200)
@@ -205,8 +207,12 @@ int dalloc(Handle* h, T** p, size_t count) {
     h->err = "hipMalloc(" + std::to_string(count * sizeof(T)) + " bytes): " + hipGetErrorString(e);
     return LCN_E_NOMEM;
   }
-  hipMemset(q, 0, std::max<size_t>(count, 1) * sizeof(T));
   h->allocs.push_back(q);
+  e = hipMemset(q, 0, std::max<size_t>(count, 1) * sizeof(T));
+  if (e != hipSuccess) {
+    h->err = std::string("hipMemset of a new allocation: ") + hipGetErrorString(e);
+    return LCN_E_HIP;
+  }
   *p = (T*)q;
   return LCN_OK;
 }
@@ -531,8 +537,13 @@ int build(Handle* h, const lcn_config* c) {
   CHECK(dalloc(h, &h->acc1, 2 * F));
   CHECK(dalloc(h, &h->acc2, 2 * F));
   CHECK(dalloc(h, &h->rowinfo, 1));
-  const size_t dw_elems = std::max((size_t)dw_chunks(h->nblk, B) * h->nblk,
-                                   (size_t)dw_chunks(h->nslab, B) * h->nslab) * 4096;
+  // chunk partials of the weight gradient, with the launch's own clamp (a chunk
+  // holds at least 64 rows): 16 KB per block and chunk -- 92 MB at the cfg3
+  // shape (175 blocks, 32 chunks), 1.2 GB at the cfg4 shape with 16 384 rows
+  // (4 624 blocks, 16 chunks)
+  auto launch_chunks = [&](int nb) { return std::max<int64_t>(1, std::min<int64_t>(dw_chunks(nb, B), cdiv(B, 64))); };
+  const size_t dw_elems = (size_t)std::max(launch_chunks(h->nblk) * h->nblk,
+                                           launch_chunks(h->nslab) * h->nslab) * 4096;
   CHECK(dalloc(h, &h->dw_part, dw_elems));
   return LCN_OK;
 }
@@ -548,6 +559,7 @@ bool multi(const Handle* h) { return has_comm(h) && !h->comm_off; }
 // In-place all-reduce of a device buffer over the ranks, stream-ordered: RCCL,
 // or (host exchange) device -> host, the caller's function, host -> device.
 int allreduce(Handle* h, void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op = ncclSum) {
+  if (h->comm_off) return LCN_OK;  // suspended: the call runs rank-locally (phased reductions included)
   if (h->comm) {
     NCCLC(ncclAllReduce(buf, buf, count, dt, op, h->comm, h->stream));
     return LCN_OK;
@@ -587,15 +599,25 @@ const RowInfo* rinfo(const Handle* h) { return multi(h) ? h->rowinfo : nullptr; 
 // lcn_set_timing: 1 = every kernel class, else bit k + 1 selects class k
 bool timed(const Handle* h, int k) { return h->timing == 1 || ((h->timing >> (k + 1)) & 1); }
 
+// A launch whose timer events cannot be created runs untimed (pair[0] stays
+// null and tstop skips it); the failure is kept for lcn_kernel_timing.
 void tstart(Handle* h, int k, hipEvent_t* pair) {
+  pair[0] = pair[1] = nullptr;
   if (!timed(h, k)) return;
   // timing-only events: no system-scope fence when they complete
-  hipEventCreateWithFlags(&pair[0], hipEventDisableSystemFence);
-  hipEventCreateWithFlags(&pair[1], hipEventDisableSystemFence);
-  hipEventRecord(pair[0], h->stream);
+  hipError_t e = hipEventCreateWithFlags(&pair[0], hipEventDisableSystemFence);
+  if (e == hipSuccess) {
+    e = hipEventCreateWithFlags(&pair[1], hipEventDisableSystemFence);
+    if (e != hipSuccess) hipEventDestroy(pair[0]);
+  }
+  if (e == hipSuccess) e = hipEventRecord(pair[0], h->stream);
+  if (e != hipSuccess) {
+    h->timer_err = std::string("kernel timer events: ") + hipGetErrorString(e);
+    pair[0] = pair[1] = nullptr;
+  }
 }
 void tstop(Handle* h, int k, hipEvent_t* pair, double flops) {
-  if (!timed(h, k)) return;
+  if (!timed(h, k) || !pair[0]) return;
   hipEventRecord(pair[1], h->stream);
   h->timers[k].ev.push_back(pair[0]);
   h->timers[k].ev.push_back(pair[1]);
@@ -652,17 +674,28 @@ int bn_stats(Handle* h, int k, int B) {
   const float* gamma = h->theta + h->gamma_off[k];
   const float* beta = h->theta + h->beta_off[k];
   const TilePartials tp = tile_partials(h, B);
+  const BnRider none{};
   if (!tp.part) launch_colreduce(h->stat_part, (int)cdiv(B, h->stat_rows), h->stat_rows, B, h->H, 1, h->colacc, s);
   if (!h->phased && !multi(h)) {
     launch_bn_fwd_finalize(h->colacc, tp, h->H, h->F, 0, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
-                           h->zsum[k], s);
+                           h->zsum[k], none, s);
     return LCN_OK;
   }
+  // several ranks: BN layer 0's all-reduce also carries the ranks' batch rows
+  // (the first exchange of a step; nothing before its finish reads RowInfo)
+  BnRider rider{};
+  if (multi(h) && k == 0) {
+    rider.kind = kRideRows;
+    rider.world = h->world;
+    rider.rank = h->rank;
+    rider.b_local = rows;
+    rider.ri_out = h->rowinfo;
+  }
   launch_bn_fwd_finalize(h->colacc, tp, h->H, h->F, 1, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
-                         h->zsum[k], s);
-  CHECK(allreduce(h, h->acc1, 2 * h->F, ncclDouble));
+                         h->zsum[k], rider, s);
+  CHECK(allreduce(h, h->acc1, 2 * h->F + rider_slots(rider), ncclDouble));
   launch_bn_fwd_finalize(h->colacc, tp, h->H, h->F, 2, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
-                         nullptr, s);
+                         nullptr, rider, s);
   return LCN_OK;
 }
 
@@ -829,17 +862,25 @@ int bn_back(Handle* h, int k, int B) {
   float* dbet = bn ? h->rg + h->beta_off[k] : nullptr;
   float* db = h->rg + h->b_off[k];
   const TilePartials tp = tile_partials(h, B);
+  const BnRider none{};
   if (!tp.part) launch_colreduce(h->stat_part, (int)cdiv(B, h->stat_rows), h->stat_rows, B, h->H, 0, h->colacc, s);
   if ((!h->phased && !multi(h)) || !bn) {
     launch_bn_bwd_finalize(h->colacc, tp, h->H, h->F, 0, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
-                           h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
+                           h->acc1, dgam, dbet, h->c123, h->zsum[k], db, none, s);
     return LCN_OK;
   }
+  // several ranks: the first BN backward of a step also carries the loss sum
+  BnRider rider{};
+  if (h->loss_pending) {
+    rider.kind = kRideLoss;
+    rider.loss = h->loss_sum;
+    h->loss_pending = false;
+  }
   launch_bn_bwd_finalize(h->colacc, tp, h->H, h->F, 1, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
-                         h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
-  CHECK(allreduce(h, h->acc1, 2 * h->F, ncclDouble));
+                         h->acc1, dgam, dbet, h->c123, h->zsum[k], db, rider, s);
+  CHECK(allreduce(h, h->acc1, 2 * h->F + rider_slots(rider), ncclDouble));
   launch_bn_bwd_finalize(h->colacc, tp, h->H, h->F, 2, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
-                         h->acc1, dgam, dbet, h->c123, h->zsum[k], db, s);
+                         h->acc1, dgam, dbet, h->c123, h->zsum[k], db, rider, s);
   return LCN_OK;
 }
 
@@ -858,7 +899,8 @@ int forward(Handle* h, int B, bool with_labels, bool train) {
   const int S = h->nslab, nl = h->nl;
   // tf.nn.dropout runs in training steps only (predict feeds rate 0, :102)
   h->drop_on = train && h->drop_rate > 0.f;
-  CHECK(exchange_rows(h, B));
+  // the ranks' batch rows: with BatchNorm they ride on BN layer 0's all-reduce (bn_stats)
+  if (!h->batch_norm) CHECK(exchange_rows(h, B));
   CHECK(prep_weights(h));
   const int epi = h->batch_norm ? EPI_BNFWD : EPI_NONE;
   // lift z0 = x . W1e + b1 (models_att.py:714-729): x padded to one 64-wide slab
@@ -1196,8 +1238,14 @@ int lcn_forward_loss(void* handle, const float* x, const float* labels, float* o
 // forward, loss, backward and update of one step, enqueued on the stream
 static int enqueue_step(Handle* h, int64_t B, bool update, bool keep) {
   CHECK(forward(h, (int)B, true, true));
-  if (multi(h)) CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
+  // the loss sum over the ranks: with BatchNorm it rides on the first BN
+  // backward's all-reduce (bn_back), else it takes an all-reduce of its own
+  if (multi(h)) {
+    if (h->batch_norm) h->loss_pending = true;
+    else CHECK(allreduce(h, h->loss_sum, 1, ncclDouble));
+  }
   CHECK(backward(h, (int)B));
+  h->loss_pending = false;
   return finish_device(h, update, keep);
 }
 
@@ -1518,6 +1566,7 @@ int lcn_comm_init(void* handle, const void* id_in, int32_t rank, int32_t world) 
   if (has_comm(h)) { h->err = "lcn_comm_init: the handle already has a communicator"; return LCN_E_ARG; }
   HIPC(hipSetDevice(h->device));
   CHECK(dalloc(h, &h->rows_all, (size_t)world));
+  CHECK(dalloc(h, &h->acc1, (size_t)2 * h->F + world + 1));  // + the riders of the SyncBN all-reduces
   // a real communicator even at world 1: every exchange below is gated on
   // h->comm, so a one-GPU run after comm_init takes the multi-GPU code path
   // (phased BN reductions, RCCL all-reduces) end to end
@@ -1535,6 +1584,7 @@ int lcn_comm_init_host(void* handle, int32_t rank, int32_t world, lcn_host_allre
   if (has_comm(h)) { h->err = "lcn_comm_init_host: the handle already has a communicator"; return LCN_E_ARG; }
   HIPC(hipSetDevice(h->device));
   CHECK(dalloc(h, &h->rows_all, (size_t)world));
+  CHECK(dalloc(h, &h->acc1, (size_t)2 * h->F + world + 1));  // + the riders of the SyncBN all-reduces
   h->host_ar = fn;
   h->host_ctx = ctx;
   h->rank = rank;
@@ -1572,6 +1622,25 @@ int lcn_comm_allreduce_host(void* handle, double* values, int32_t count, int32_t
   return LCN_OK;
 }
 
+int lcn_comm_info(void* handle, int32_t* kind, int32_t* rank, int32_t* world) {
+  Handle* h = (Handle*)handle;
+  if (!h) return LCN_E_ARG;
+  int k = LCN_COMM_NONE, r = 0, w = 1;
+  if (h->comm) {
+    k = LCN_COMM_RCCL;
+    NCCLC(ncclCommUserRank(h->comm, &r));
+    NCCLC(ncclCommCount(h->comm, &w));
+  } else if (h->host_ar) {
+    k = LCN_COMM_HOST;
+    r = h->rank;
+    w = h->world;
+  }
+  if (kind) *kind = k;
+  if (rank) *rank = r;
+  if (world) *world = w;
+  return LCN_OK;
+}
+
 int lcn_set_timing(void* handle, int32_t enable) {
   Handle* h = (Handle*)handle;
   if (!h) return LCN_E_ARG;
@@ -1580,6 +1649,7 @@ int lcn_set_timing(void* handle, int32_t enable) {
     for (auto e : t.ev) hipEventDestroy(e);
     t = Timer();
   }
+  h->timer_err.clear();
   h->timing = enable;
   return LCN_OK;
 }
@@ -1588,6 +1658,7 @@ int lcn_kernel_timing(void* handle, int32_t k, int64_t* launches, double* total_
   Handle* h = (Handle*)handle;
   if (!h || k < 0 || k >= LCN_K_NUM) return LCN_E_ARG;
   HIPC(hipStreamSynchronize(h->stream));
+  if (!h->timer_err.empty()) { h->err = h->timer_err; return LCN_E_HIP; }
   Timer& t = h->timers[k];
   double ms = 0.0;
   for (size_t i = 0; i + 1 < t.ev.size(); i += 2) {

@@ -240,6 +240,22 @@ void launch_colreduce(const float2* part, int n_tiles, int tile_rows, int B, int
 struct TilePartials {
   const float2* part; int n_tiles, tile_rows, B;
 };
+// Values that ride on a SyncBN all-reduce, appended to its 2F channel sums at
+// acc[2F ..], so a data-parallel step needs no collective of their own:
+//   kRideRows (forward, BN layer 0): the ranks' batch rows, one slot per rank
+//     (phase 1 fills this rank's slot, the all-reduce sums the one-hot vectors,
+//     phase 2 derives this rank's RowInfo and uses the global row count);
+//   kRideLoss (the first BN backward of a step): the rank's loss sum, one slot
+//     (phase 1 reads *loss, phase 2 writes the all-reduced sum back).
+enum { kRideNone = 0, kRideRows = 1, kRideLoss = 2 };
+struct BnRider {
+  int kind;
+  int world, rank;      // kRideRows
+  double b_local;       // kRideRows: this rank's batch rows
+  RowInfo* ri_out;      // kRideRows: written by phase 2
+  double* loss;         // kRideLoss
+};
+inline int rider_slots(const BnRider& r) { return r.kind == kRideRows ? r.world : r.kind == kRideLoss ? 1 : 0; }
 // forward BN finish from colreduce mode-1 sums.  phase 0 complete (single GPU);
 // 1 local channel sums -> acc[2F]; 2 finish from all-reduced acc.  The element
 // count per channel is rows_global * J, rows_global = `rows` or, when ri is
@@ -247,13 +263,14 @@ struct TilePartials {
 void launch_bn_fwd_finalize(const double2* col, const TilePartials& tp, int H, int F, int phase,
                             double rows, const RowInfo* ri,
                             const float* gamma, const float* beta, float eps, double* acc,
-                            BnStats st, double* zsum, hipStream_t s);
+                            BnStats st, double* zsum, const BnRider& rider, hipStream_t s);
 // backward BN finish from colreduce mode-0 sums of (du, du*zhat): c1|c2|c3,
 // local dgamma/dbeta and the bias gradient db; bn = 0: db = sum du only
 void launch_bn_bwd_finalize(const double2* col, const TilePartials& tp, int H, int F, int phase,
                             int bn, double rows, const RowInfo* ri, double b_local, const float* gamma, const float* mean,
                             const float* rstd, double* acc, float* dgamma, float* dbeta,
-                            float* c123, const double* zsum, float* db, hipStream_t s);
+                            float* c123, const double* zsum, float* db, const BnRider& rider,
+                            hipStream_t s);
 // h = [res +] leaky(scale*z + shift), tiled [B][S*64] buffers
 void launch_bn_act(const float* z, const float* res, float* h, const float* scale,
                    const float* shift, int F, float alpha, int B, int S, const Dropout& drop,

@@ -16,9 +16,18 @@ e.g. all on one GPU):
 from __future__ import annotations
 
 import os
+import sys
+import threading
 import time
 
 from lcn_amd import native
+
+
+def bootstrap_timeout():
+    """Seconds a rank may spend joining the communicator (LCN_BOOTSTRAP_TIMEOUT,
+    default 120): waiting for rank 0's id file and inside ncclCommInitRank, which
+    has no bound of its own."""
+    return float(os.environ.get("LCN_BOOTSTRAP_TIMEOUT", "120"))
 
 
 def dist_env():
@@ -59,10 +68,10 @@ def exchange_uid(rank, world):
             f.write(uid)
         os.replace(tmp, path)
         return uid
-    t0 = time.time()
+    t0, limit = time.time(), bootstrap_timeout()
     while not os.path.exists(path):
-        if time.time() - t0 > 300:
-            raise RuntimeError("timed out waiting for the RCCL unique id")
+        if time.time() - t0 > limit:
+            raise RuntimeError(f"rank {rank}: no RCCL unique id from rank 0 within {limit:.0f} s ({path})")
         time.sleep(0.05)
     time.sleep(0.05)
     with open(path, "rb") as f:
@@ -85,19 +94,62 @@ def gloo_allreduce(rank, world):
     return allreduce
 
 
+class BootstrapWatchdog:
+    """Ends this process (exit code 86, a line on stderr) if the block it guards
+    has not finished within `seconds`: ncclCommInitRank and the first
+    collective wait for every rank without a bound, so one rank that never
+    arrives would otherwise hang all the others until the launcher's own limit.
+    The launcher (bench.py's spawner, torch.distributed.run) sees the failed
+    rank and stops the rest."""
+
+    def __init__(self, rank, seconds, what="communicator setup"):
+        self.rank, self.seconds, self.what = rank, seconds, what
+        self.timer = None
+
+    def _abort(self):
+        sys.stderr.write(f"lcn: rank {self.rank} did not complete the {self.what} within "
+                         f"{self.seconds:.0f} s (LCN_BOOTSTRAP_TIMEOUT); exiting\n")
+        sys.stderr.flush()
+        os._exit(86)
+
+    def __enter__(self):
+        if self.seconds > 0:
+            self.timer = threading.Timer(self.seconds, self._abort)
+            self.timer.daemon = True
+            self.timer.start()
+        return self
+
+    def __exit__(self, *exc):
+        if self.timer is not None:
+            self.timer.cancel()
+        return False
+
+
+def mark_ready(rank):
+    """Tell a parent that started the ranks (bench.py's spawner sets
+    LCN_READY_DIR) that this rank holds its communicator."""
+    d = os.environ.get("LCN_READY_DIR")
+    if d:
+        with open(os.path.join(d, f"ready{rank}"), "w") as f:
+            f.write("ok\n")
+
+
 def comm_setup(net, rank, world):
     """RCCL communicator over the node's ranks; once every rank holds it (the
     host all-reduce below is its first collective) rank 0 removes the id
     file, so a later launch can never read a stale id.  LCN_COMM=gloo: the
-    host-exchange communicator over gloo instead."""
-    if os.environ.get("LCN_COMM", "rccl") == "gloo":
-        net.comm_init_host(rank, world, gloo_allreduce(rank, world))
-        net.allreduce_host([0.0])
-        return
-    net.comm_init(exchange_uid(rank, world), rank, world)
-    net.allreduce_host([0.0])
-    if rank == 0:
-        try:
-            os.remove(uid_path())
-        except OSError:
-            pass
+    host-exchange communicator over gloo instead.  The whole setup is bounded
+    by bootstrap_timeout() (BootstrapWatchdog)."""
+    with BootstrapWatchdog(rank, bootstrap_timeout()):
+        if os.environ.get("LCN_COMM", "rccl") == "gloo":
+            net.comm_init_host(rank, world, gloo_allreduce(rank, world))
+            net.allreduce_host([0.0])
+        else:
+            net.comm_init(exchange_uid(rank, world), rank, world)
+            net.allreduce_host([0.0])
+            if rank == 0:
+                try:
+                    os.remove(uid_path())
+                except OSError:
+                    pass
+    mark_ready(rank)

@@ -87,6 +87,7 @@ SIGNATURES = {
     "lcn_comm_init_host": ([_vp, _i32, _i32, HOST_ALLREDUCE_FN, _vp], _i32),
     "lcn_comm_suspend": ([_vp, _i32], _i32),
     "lcn_comm_allreduce_host": ([_vp, _f64p, _i32, _i32], _i32),
+    "lcn_comm_info": ([_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32), ctypes.POINTER(_i32)], _i32),
     "lcn_crc32c": ([ctypes.c_uint32, ctypes.c_char_p, _i64], ctypes.c_uint32),
     "lcn_set_dropout": ([_vp, ctypes.c_float, ctypes.c_uint64], _i32),
     "lcn_eval_mpjpe": ([_i32, _i64, _f64p, _f64p, _f64p, _f64p, _f64p, _i32, _f64p], _i32),
@@ -413,6 +414,13 @@ class Network:
         self._check(self.lib.lcn_comm_allreduce_host(self.h, v.ctypes.data_as(_f64p), v.size,
                                                      1 if op == "max" else 0))
         return v
+
+    def comm_info(self):
+        """(kind, rank, world) of the handle's communicator as it reports them
+        itself (lcn_comm_info): kind "none" / "rccl" / "host"."""
+        k, r, w = _i32(), _i32(), _i32()
+        self._check(self.lib.lcn_comm_info(self.h, ctypes.byref(k), ctypes.byref(r), ctypes.byref(w)))
+        return ("none", "rccl", "host")[k.value], r.value, w.value
 
     # -- instrumentation
     def set_dropout(self, rate: float, seed: int = 0):

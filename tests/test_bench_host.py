@@ -86,6 +86,12 @@ rec = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTE
 rec["argv"] = sys.argv[1:]
 with open(os.path.join(out, "rank%s.json" % rec["RANK"]), "w") as f:
     json.dump(rec, f)
+if os.environ.get("STUB_HANG_RANK") == rec["RANK"]:
+    print("stub rank %s: waiting for a peer that never comes" % rec["RANK"], file=sys.stderr, flush=True)
+    time.sleep(60)   # never reports its communicator
+if os.environ.get("STUB_HANG_RANK") is not None:
+    open(os.path.join(os.environ["LCN_READY_DIR"], "ready" + rec["RANK"]), "w").close()
+    time.sleep(60)   # holds its communicator and waits in the first collective
 if os.environ.get("STUB_FAIL_RANK") == rec["RANK"]:
     sys.exit(3)
 if os.environ.get("STUB_FAIL_RANK") is not None:
@@ -126,6 +132,54 @@ def test_a_failing_rank_fails_the_run_and_stops_the_others(tmp_path, monkeypatch
     assert time.time() - t0 < 30   # the other ranks were stopped, not waited for
 
 
+def test_a_rank_that_never_joins_is_stopped_with_its_stderr_tail(tmp_path, monkeypatch, capfd):
+    """One rank never reports its communicator: after the bound the spawner stops
+    every rank, fails, and shows what each rank last wrote to stderr."""
+    import time
+    stub = tmp_path / "rank_stub.py"
+    stub.write_text(RANK_STUB)
+    monkeypatch.setenv("STUB_OUT", str(tmp_path))
+    monkeypatch.setenv("STUB_HANG_RANK", "1")
+    monkeypatch.setenv("LCN_SPAWN_READY_TIMEOUT", "1.5")
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    argv = ["--gpus", "3", "--steps", "2"]
+    t0 = time.time()
+    assert bench.spawn_ranks(bench.parse(argv), argv, script=str(stub)) != 0
+    assert time.time() - t0 < 30
+    err = capfd.readouterr().err
+    assert "rank(s) [1] had no communicator" in err
+    assert "[rank 1] stub rank 1: waiting for a peer that never comes" in err
+
+
+def test_bootstrap_watchdog_ends_a_rank_stuck_in_the_setup(tmp_path):
+    """dist.BootstrapWatchdog: a communicator setup that does not return (as
+    ncclCommInitRank does when a peer is missing) ends the process with exit
+    code 86 and a line on stderr; a setup that returns in time is left alone."""
+    import subprocess
+    import time
+    code = (
+        "import sys, time\n"
+        f"sys.path.insert(0, {os.path.join(REPO, 'lcn-pose_amd')!r})\n"
+        "from lcn_amd import dist\n"
+        "with dist.BootstrapWatchdog(3, float(sys.argv[1])):\n"
+        "    time.sleep(float(sys.argv[2]))\n"
+        "print('setup done')\n")
+    t0 = time.time()
+    hung = subprocess.run([sys.executable, "-c", code, "0.5", "60"], capture_output=True, text=True, timeout=60)
+    assert hung.returncode == 86 and time.time() - t0 < 30
+    assert "rank 3 did not complete the communicator setup" in hung.stderr
+    ok = subprocess.run([sys.executable, "-c", code, "30", "0.1"], capture_output=True, text=True, timeout=60)
+    assert ok.returncode == 0 and "setup done" in ok.stdout
+
+
+def test_uid_wait_is_bounded(monkeypatch):
+    """A rank whose rank 0 never publishes the id gives up after LCN_BOOTSTRAP_TIMEOUT."""
+    monkeypatch.setenv("MASTER_PORT", str(40002 + os.getpid() % 20000))
+    monkeypatch.setenv("LCN_BOOTSTRAP_TIMEOUT", "0.3")
+    with pytest.raises(RuntimeError, match="no RCCL unique id"):
+        bench.exchange_uid(1, 2)
+
+
 def test_world_size_must_match_gpus(monkeypatch, capsys):
     monkeypatch.setenv("WORLD_SIZE", "2")
     monkeypatch.setenv("RANK", "0")
@@ -142,6 +196,8 @@ def test_batch_plan_strong_and_weak():
     assert [bench.batch_plan(a, 3, r)[0] for r in range(3)] == [334, 333, 333]
     a = bench.parse(["--batch", "4096"])
     assert bench.batch_plan(a, 4, 2) == (4096, 16384, "weak")
+    a = bench.parse(["--config", "cfg2"])
+    assert a.mode == "forward" and (a.knn, a.layers, a.channels, a.global_batch) == (3, 3, 64, 65536)
     a = bench.parse(["--config", "cfg4"])
     assert (a.mask_type, a.layers, a.channels, a.global_batch) == ("exponential", 6, 256, 131072)
     a = bench.parse(["--config", "cfg5"])

@@ -140,3 +140,44 @@ def test_predict_tta_matches_host_concatenation(model_dir):
     got = model.predict_tta(x, flip=True, rotate=True, sess=net)
     assert np.abs(got - ref).max() <= 1e-5
     assert np.mean(np.abs(got - ref) <= 1e-12) > 0.99
+
+
+def test_initialiser_on_the_librarys_own_layout():
+    """init_flat fed from Network.param_layout() -- what cgcnn and bench.py do:
+    the layout's names / offsets / shapes are the oracle's variable order, a
+    bias comes out rank 1 (so cgcnn.kaiming's shape[0] is its own length,
+    models_att.py:614-628: scale sqrt(2 / n), not sqrt(2)), and what is set is
+    what the device holds."""
+    import math
+    import re
+
+    import lcn_oracle as O
+    from lcn_amd.init import init_flat
+    from lcn_testutil import make_cfg, make_network
+    cfg = make_cfg(F=64, L=2, knn=3)
+    net = make_network(cfg, max_batch=32)
+    layout = net.param_layout()
+    off = 0
+    for (name, o, shape), (oname, oshape) in zip(layout, O.param_specs(cfg)):
+        assert (name, o, tuple(shape)) == (oname, off, tuple(oshape))
+        off += int(np.prod(shape))
+    assert off == net.n_params and len(layout) == len(O.param_specs(cfg))
+    nb = O.neighbour_matrix(3)
+    flat = init_flat(layout, net.n_params, nb, seed=5)
+    n_bias = 0
+    for name, o, shape in layout:
+        v = flat[o:o + int(np.prod(shape))]
+        if re.match(r"b\d", name):       # b1, b2_l, b3_l, b4 (not the bn* affine pairs)
+            assert len(shape) == 1, (name, shape)
+            s = math.sqrt(2.0 / shape[0])
+            assert np.abs(v).max() <= 2.0 * s * (1 + 1e-6), name          # truncated at 2 sigma
+            tol = 0.25 if v.size < 500 else 0.06
+            assert abs(v.std() / (s * math.sqrt(0.77374)) - 1) < tol, (name, v.std(), s)
+            n_bias += 1
+        elif re.match(r"w\d", name):
+            s = math.sqrt(2.0 / shape[0])
+            assert len(shape) == 2 and np.abs(v).max() <= 2.0 * s * (1 + 1e-6), name
+    assert n_bias == 2 * cfg.num_layers + 2
+    net.set_params(flat)
+    np.testing.assert_array_equal(net.get_params(), flat)
+    net.close()

@@ -75,7 +75,16 @@ CASES = {
     "lc_knn3": dict(F=64, L=2, knn=3),
     "lc_knn1_nores": dict(F=64, L=1, knn=1, residual=False),
     "exp_reg": dict(F=64, L=1, mask="exponential", regularization=1e-3),
+    # several 64-feature slabs per joint: the phased SyncBN finish folds the
+    # slabs of a joint into channels (spj = 2 and 4)
+    "lc_F128": dict(F=128, L=1, knn=2),
+    "cfg4_shape": dict(F=256, L=2, knn=2, mask="exponential"),
 }
+# The wide cases are held to the one-handle run only (1e-5: their float32 sums
+# are split differently); the one-handle path itself is checked against the
+# float64 oracle at these shapes, with LeakyReLU kink handling, in
+# tests/test_gpu_parity.py.
+WIDE = {"lc_F128", "cfg4_shape"}
 
 
 @pytest.mark.parametrize("case,sizes", [
@@ -83,7 +92,10 @@ CASES = {
     ("lc_knn3", [77, 45]),            # ragged 32-row tiles, uneven shards
     ("lc_knn1_nores", [40, 33, 55]),  # three ranks
     ("exp_reg", [96, 32]),
-], ids=["equal2", "ragged2", "three", "exp_reg"])
+    ("lc_F128", [48, 48]),
+    ("cfg4_shape", [48, 48]),
+    ("cfg4_shape", [50, 46]),
+], ids=["equal2", "ragged2", "three", "exp_reg", "F128", "cfg4_equal2", "cfg4_ragged2"])
 def test_sharded_step_equals_full_batch(case, sizes):
     world, B = len(sizes), sum(sizes)
     cfg = make_cfg(**CASES[case])
@@ -123,30 +135,108 @@ def test_sharded_step_equals_full_batch(case, sizes):
     one.close()
 
     # (b) float64 oracle
+    wide = case in WIDE
+    tol = 1e-5 if wide else 1e-6
     out64, cache = O.forward(cfg, params, x, np.float64)
-    g64 = O.backward(cfg, params, cache, lab, np.float64)
     loss64 = O.mse_loss(out64, lab) + O.reg_loss(cfg, params)
+    g64 = None if wide else O.backward(cfg, params, cache, lab, np.float64)
 
     for r in range(world):
         sl = slice(offs[r], offs[r + 1])
         got = res[r]
-        assert np.abs(got["out"] - out1[sl]).max() <= 1e-6
+        assert np.abs(got["out"] - out1[sl]).max() <= tol
         assert np.abs(got["out"] - out64[sl]).max() <= 1e-4
         # every rank reports the loss of the whole batch
         for k, ref in (("floss", floss1), ("loss", loss1), ("l1", l11), ("l2", l12)):
-            assert abs(got[k] - ref) <= 1e-6 * max(1.0, abs(ref)), (k, got[k], ref)
+            assert abs(got[k] - ref) <= tol * max(1.0, abs(ref)), (k, got[k], ref)
         assert abs(got["loss"] - loss64) <= 1e-6 + 1e-5 * abs(loss64)
         # the all-reduced gradient, identical on every rank
         np.testing.assert_array_equal(got["grads"], res[0]["grads"])
         gr, g1u = O.unflatten(cfg, got["grads"]), O.unflatten(cfg, g1)
         for name, _ in O.param_specs(cfg):
-            assert rel_err(gr[name], g1u[name]) <= 1e-6, name
-            assert rel_err(gr[name], g64[name]) <= 1e-4, name
+            assert rel_err(gr[name], g1u[name]) <= tol, name
+            if g64 is not None:
+                assert rel_err(gr[name], g64[name]) <= 1e-4, name
         # two Adam steps: replicas stay identical and follow the one-handle run
         np.testing.assert_array_equal(got["theta"], res[0]["theta"])
-        assert np.abs(got["theta"] - theta1).max() <= 1e-6
+        assert np.abs(got["theta"] - theta1).max() <= tol
     # the ranks made the same number of exchanges
     assert len(set(ar.calls)) == 1
+
+
+@pytest.mark.parametrize("L", [0, 1, 3])
+def test_collectives_per_step(L):
+    """A data-parallel training step makes 4L + 3 exchanges: one SyncBN
+    all-reduce per BN layer forward (1 + 2L; layer 0's also carries the ranks'
+    batch rows) and backward (1 + 2L; the first also carries the loss sum), and
+    one of the raw gradient vector.  forward_loss: 1 + 2L and the loss."""
+    sizes, world = [40, 56], 2
+    cfg = make_cfg(F=64, L=L, knn=2)
+    flat = O.flatten(cfg, perturbed_params(cfg, seed=4))
+    x, lab = synthetic_batch(sum(sizes), seed=9)
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    ar = ThreadAllReduce(world)
+
+    def rank_fn(r):
+        net = make_network(cfg, max_batch=max(sizes))
+        net.comm_init_host(r, world, ar.for_rank(r))
+        net.set_params(flat)
+        sl = slice(offs[r], offs[r + 1])
+        assert net.comm_info() == ("host", r, world)
+        c0 = ar.calls[r]
+        loss, _ = net.train_step(x[sl], lab[sl])
+        c1 = ar.calls[r]
+        net.forward_loss(x[sl], lab[sl])
+        c2 = ar.calls[r]
+        net.forward(x[sl])
+        c3 = ar.calls[r]
+        net.close()
+        return c1 - c0, c2 - c1, c3 - c2, loss
+
+    res = run_ranks(world, rank_fn)
+    for step_calls, floss_calls, fwd_calls, _ in res:
+        assert step_calls == 4 * L + 3
+        assert floss_calls == 2 * L + 2
+        assert fwd_calls == 2 * L + 1
+    assert res[0][3] == res[1][3]
+
+
+def test_suspended_calls_make_no_exchange_with_phased_reductions(monkeypatch):
+    """With the phased (multi-GPU) BN reductions forced on, a suspended
+    communicator keeps every exchange off: ranks predict different numbers of
+    batches rank-locally (no deadlock, no all-reduce call) and get the
+    one-handle results."""
+    monkeypatch.setenv("LCN_FORCE_PHASED", "1")
+    world, bs = 2, 32
+    cfg = make_cfg(F=64, L=1, knn=2)
+    flat = O.flatten(cfg, perturbed_params(cfg, seed=6))
+    x, _ = synthetic_batch(3 * bs, seed=8)
+    rows = [x[:2 * bs], x[2 * bs:]]       # two batches on rank 0, one on rank 1
+    ar = ThreadAllReduce(world)
+
+    def rank_fn(r):
+        net = make_network(cfg, max_batch=bs)
+        net.comm_init_host(r, world, ar.for_rank(r))
+        net.set_params(flat)
+        net.comm_suspend(True)
+        c0 = ar.calls[r]
+        net.dataset_upload(0, rows[r].astype(np.float64))
+        p = net.predict_dataset(0, rows[r].shape[0], bs)
+        calls = ar.calls[r] - c0
+        net.comm_suspend(False)
+        net.close()
+        return p, calls
+
+    res = run_ranks(world, rank_fn)
+    monkeypatch.delenv("LCN_FORCE_PHASED")
+    one = make_network(cfg, max_batch=bs)
+    one.set_params(flat)
+    for r in range(world):
+        assert res[r][1] == 0
+        one.dataset_upload(0, rows[r].astype(np.float64))
+        ref = one.predict_dataset(0, rows[r].shape[0], bs)
+        assert np.abs(res[r][0] - ref).max() <= 1e-6
+    one.close()
 
 
 def test_dropout_masks_follow_the_global_row():

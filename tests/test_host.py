@@ -142,3 +142,33 @@ def test_env_overrides_pick_device_and_transport(monkeypatch):
     assert dist.dist_env() == (3, 4, 3)
     monkeypatch.setenv("LCN_DEVICE", "0")
     assert dist.dist_env() == (3, 4, 0)
+
+
+def test_cli_flag_table_matches_the_reference_schema():
+    """tools/cli_flags.py: flags, defaults, choices and required-ness of the
+    two CLIs as the reference declares them (train.py:16-40, inference.py:16-40)."""
+    from tools import cli_flags
+    train = vars(cli_flags.parse("train", ["--train_set", "h36m", "--validation_set", "mpii"]))
+    assert train == dict(
+        test_indices="1", mask_type="locally_connected", init_type="same", knn=2, layers=3, dropout=0,
+        channels=64, subset=None, epochs=25, batch_size=200, learning_rate=0.001, regularization=None,
+        in_F=2, flip_data=False, rotation_data=False, translate_data=False, translation_factor=0.1,
+        rotation_factor=60, resume_from=None, output_file=None, train_set="h36m",
+        validation_set="mpii", test_set=None, n_test=1)
+    inf = vars(cli_flags.parse("inference", ["--train_set", "h36m", "--test_set", "humansc3d"]))
+    assert inf == dict(
+        test_indices="1", mask_type="locally_connected", init_type="same", graph=0, knn=2, layers=3,
+        in_joints=17, out_joints=17, dropout=0.25, channels=64, subset=None, epochs=200,
+        checkpoints=None, batch_size=200, regularization=None, learning_rate=0.001, in_F=2,
+        flip_data=False, rotation_data=False, translate_data=False, translation_factor=0.1,
+        train_set="h36m", test_set="humansc3d")
+    for prog, argv in (("train", ["--train_set", "h36m"]),                       # --validation_set required
+                       ("inference", ["--train_set", "h36m"]),                   # --test_set required
+                       ("train", ["--train_set", "h36m", "--validation_set", "h36m", "--init-type", "ones"]),
+                       ("train", ["--train_set", "h36m", "--validation_set", "h36m", "--checkpoints", "best"]),
+                       ("inference", ["--train_set", "x", "--test_set", "h36m"])):
+        with pytest.raises(SystemExit):
+            cli_flags.parse(prog, argv)
+    ok = cli_flags.parse("inference", ["--train_set", "h36m", "--test_set", "h36m", "--init-type", "random",
+                                       "--checkpoints", "best", "--flip-data", "--in-F", "3"])
+    assert (ok.init_type, ok.checkpoints, ok.flip_data, ok.in_F) == ("random", "best", True, 3)
