@@ -112,9 +112,9 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&Y, (size_t)B * H * 4));
   float2* stat;
   CK(hipMalloc(&stat, (size_t)(B / 32 + 1) * H * 8 + (size_t)B * 17));
-  const int nch = std::max(1, std::min(64, 8192 / nblk));
+  const int nch = std::getenv("LCN_DW_NCH") ? std::atoi(std::getenv("LCN_DW_NCH")) : std::max(1, std::min(64, 5600 / nblk));
   float* part;
-  CK(hipMalloc(&part, (size_t)nch * nblk * 4096 * 4));
+  CK(hipMalloc(&part, (size_t)128 * nblk * 4096 * 4));
   float* dW;
   CK(hipMalloc(&dW, (size_t)H * H * 4));
   hipStream_t s;
@@ -175,13 +175,14 @@ int main(int argc, char** argv) {
   d.d_shift = sh;
   d.d_c123 = c123;
   d.d_F = F;
+  std::vector<int4> dw_map_host;
   std::vector<int4> grp;  // as lcn_api.cpp upload_dw_groups
   for (int so = 0; so < J; ++so) {
     std::vector<int> ids;
     for (int b = 0; b < nblk; ++b)
       if (blk[b].y == so) ids.push_back(b);
     for (size_t i = 0; i < ids.size(); i += 2)
-      grp.push_back(make_int4(so, ids[i], i + 1 < ids.size() ? ids[i + 1] : -1, i == 0 ? 1 : 0));
+      grp.push_back(make_int4(so, ids[i], i + 1 < ids.size() ? ids[i + 1] : -1, (int)(i / 2) | ((int)((ids.size() + 1) / 2) << 8)));
   }
   d.groups = dev(grp);
   d.ngroups = (int)grp.size();
@@ -191,8 +192,18 @@ int main(int argc, char** argv) {
   d.blk = dblk;
   d.nblk = nblk;
   d.B = B;
-  d.chunk_rows = ((B + nch - 1) / nch + 63) / 64 * 64;
-  d.nchunks = (B + d.chunk_rows - 1) / d.chunk_rows;
+  {
+    const int slots = std::getenv("LCN_DW_SLOTS") ? std::atoi(std::getenv("LCN_DW_SLOTS")) : gemm_dw_resident_slots();
+    d.plan = make_dw_plan(B, (int)grp.size(), slots, nch, 128);
+    if (std::getenv("LCN_DW_ITEM")) d.plan.item_rows = std::atoi(std::getenv("LCN_DW_ITEM"));
+    if (std::getenv("LCN_DW_ROUNDS") && d.plan.stride == 8) d.plan.n_slots = 8 * d.plan.sub * std::atoi(std::getenv("LCN_DW_ROUNDS"));
+    const std::vector<int4> map = make_dw_wgmap((int)grp.size(), d.plan, B);
+    dw_map_host = map;
+    d.wgmap = dev(map);
+    d.n_wg = (int)map.size();
+    std::printf("dw plan: items of %d rows, stride %d, %d partials per block, %d workgroups (resident slots %d)\n",
+                d.plan.item_rows, d.plan.stride, d.plan.n_slots, d.n_wg, slots);
+  }
   d.part = part;
 
   struct Case { const char* name; int kind; int pro; int variant; };
@@ -223,7 +234,7 @@ int main(int argc, char** argv) {
           d.pro_shift = c.pro == PRO_BNACT ? sh : nullptr;
           d.d_bnback = c.pro != PRO_RAW;
           launch_gemm_dw(d, s);
-          launch_dw_reduce(part, d.nchunks, nblk, dblk, dW, H, H, H, s);
+          launch_dw_reduce(part, dw_plan_slots(d.plan), nblk, dblk, dW, H, H, H, s);
         } else {
           launch_gemm_bs(mk(c.kind, c.pro, c.variant), s);
         }
@@ -242,6 +253,65 @@ int main(int argc, char** argv) {
     }
   }
 #ifdef EXP_CLOCK
+  for (int mode = 0; mode < 3; ++mode) {  // in-kernel clock and residency of the weight-gradient GEMM (raw; BN-backward D; + BN-apply A)
+    const int grid = d.n_wg;
+    uint64_t* clk;
+    CK(hipMalloc(&clk, (size_t)grid * 32));
+    d.clk = clk;
+    d.pro_scale = mode == 2 ? sc : nullptr;
+    d.pro_shift = mode == 2 ? sh : nullptr;
+    d.d_bnback = mode >= 1;
+    for (int it = 0; it < 1200; ++it) launch_gemm_dw(d, s);
+    CK(hipStreamSynchronize(s));
+    std::vector<uint64_t> st((size_t)4 * grid);
+    CK(hipMemcpy(st.data(), clk, st.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<double> ghz, life;
+    uint64_t t0 = ~0ull, t1 = 0;
+    CK(hipMemset(clk, 0, (size_t)grid * 32));
+    launch_gemm_dw(d, s);
+    CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(st.data(), clk, st.size() * 8, hipMemcpyDeviceToHost));
+    for (int i = 0; i < grid; ++i) {
+      if (st[4 * i + 3] == 0) continue;  // padding workgroups leave no stamps
+      if (st[4 * i + 1] > 100) ghz.push_back((double)st[4 * i] / (double)st[4 * i + 1] * 0.1);
+      life.push_back((double)st[4 * i + 1] * 0.01);
+      t0 = std::min(t0, st[4 * i + 2]);
+      t1 = std::max(t1, st[4 * i + 3]);
+    }
+    std::sort(ghz.begin(), ghz.end());
+    std::sort(life.begin(), life.end());
+    std::printf("dw mode %d: in-kernel clock (GHz) min %.3f median %.3f max %.3f; launch span %.1f us; workgroup life (us) min %.1f median %.1f max %.1f; resident per 5%% bin:",
+                mode, ghz.front(), ghz[ghz.size() / 2], ghz.back(), (double)(t1 - t0) * 0.01, life.front(),
+                life[life.size() / 2], life.back());
+    const double span = (double)(t1 - t0);
+    std::vector<double> act(20, 0.0);
+    for (int i = 0; i < grid; ++i) {
+      if (st[4 * i + 3] == 0) continue;
+      const double b0 = (st[4 * i + 2] - t0) / span * 20, b1 = (st[4 * i + 3] - t0) / span * 20;
+      for (int b = (int)b0; b < 20 && b <= (int)b1; ++b)
+        act[b] += std::min(b1, (double)b + 1) - std::max(b0, (double)b);
+    }
+    for (double v : act) std::printf(" %.0f", v);
+    {  // median life by kind of slot: XCD-affine (j < 8) / dealt (j >= 8) two-block, one-block; and by XCD
+      std::vector<double> cat[3], byx[8];
+      for (int i = 0; i < grid; ++i) {
+        if (st[4 * i + 3] == 0 || dw_map_host[i].x < 0) continue;
+        const double l = (double)st[4 * i + 1] * 0.01;
+        const bool two = grp[dw_map_host[i].x].z >= 0;
+        cat[!two ? 2 : dw_map_host[i].y < 8 ? 0 : 1].push_back(l);  // first round / later rounds / one-block
+        if (two) byx[i & 7].push_back(l);
+      }
+      std::printf("; median life affine/dealt/one-block:");
+      for (auto& c : cat) { std::sort(c.begin(), c.end()); std::printf(" %.0f", c.empty() ? 0.0 : c[c.size() / 2]); }
+      std::printf("; by XCD:");
+      for (auto& c : byx) { std::sort(c.begin(), c.end()); std::printf(" %.0f", c.empty() ? 0.0 : c[c.size() / 2]); }
+    }
+    std::printf("; life deciles:");
+    for (int q = 0; q <= 10; ++q) std::printf(" %.0f", life[std::min(life.size() - 1, life.size() * q / 10)]);
+    std::printf("\n");
+    d.clk = nullptr;
+    CK(hipFree(clk));
+  }
   {  // in-kernel clock of the no-epilogue forward GEMM after sustained load,
      // and the occupancy profile of its last launch (how long the tail is)
     GemmArgs a = mk(3, PRO_RAW, 0);

@@ -9,14 +9,15 @@
 namespace lcn {
 
 // One workgroup = a group of up to two 64x64 blocks (si0, so), (si1, so) x
-// one batch chunk; waves (bi, hp) = (w >> 1, w & 1) compute rows 32hp..+31 of
+// one slot of the batch (DwPlan: a strided set of row items); waves (bi, hp) = (w >> 1, w & 1) compute rows 32hp..+31 of
 // block bi against all 64 columns (two 32x32 accumulators), so the staged D
 // slab -- and its BN-backward rebuild -- serves both blocks.  A group of one
 // block (the last of an output slab with an odd number of blocks) splits the
 // block four ways instead, wave (qh, hp) = (w >> 1, w & 1) computing rows
 // 32hp..+31 x columns 32qh..+31 in one accumulator: half the MFMAs per stage,
-// no idle wave.  One 32-row tile per LDS stage.  Work ids are chunk-major so the groups of one chunk (same
-// batch rows) run on one XCD and share the activation tiles through its L2.
+// no idle wave.  One 32-row tile per LDS stage.  The slots are placed by XCD
+// (make_dw_wgmap) so the groups that read the same rows at the same time share
+// the activation tiles through that XCD's L2.
 //
 // Staging: every thread loads 2 float4 of each operand's 8 KB row-tile slab
 // (coalesced 1 KB chunks), applies the operand transform (channel constants
@@ -27,8 +28,8 @@ namespace lcn {
 //
 // PRO: the A operand gets BN apply + LeakyReLU (A = z of the layer below the
 // block's inner layer); DBB: the D operand is dz rebuilt from (dh, z) by the
-// BN + LeakyReLU backward, dz = c1 du + c2 + c3 z; one group per output slab
-// also stores that dz (dz_out) for the backward-data GEMM that follows, so dz
+// BN + LeakyReLU backward, dz = c1 du + c2 + c3 z; the groups of an output slab
+// take turns storing that dz (dz_out) for the backward-data GEMM that follows, so dz
 // costs one write and no separate elementwise pass.
 constexpr int kDwLd = 36;
 
@@ -38,8 +39,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   __shared__ __attribute__((aligned(16))) float As[2][64 * kDwLd];   // [p][row] per block
   // channel constants: A sc, sh of si0; A sc, sh of si1; D sc, sh, c1, c2, c3
   __shared__ __attribute__((aligned(16))) float tab[9 * 64];
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int chunk = wg / a.ngroups, gi = wg - chunk * a.ngroups;
+#ifdef EXP_CLOCK
+  const uint64_t ck0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  // Work map (DwPlan, make_dw_wgmap): this workgroup's group of blocks, its
+  // partial slot, and its items item0, item0 + stride, ... (n_it of them), all
+  // accumulated in registers.
+  const DwPlan pl = a.plan;
+  const int4 wgm = a.wgmap[blockIdx.x];
+  const int gi = __builtin_amdgcn_readfirstlane(wgm.x), slot = __builtin_amdgcn_readfirstlane(wgm.y);
+  const int item0 = __builtin_amdgcn_readfirstlane(wgm.z), n_it = __builtin_amdgcn_readfirstlane(wgm.w);
+  if (gi < 0) return;  // padding of the grid (uniform per workgroup)
   const int4 grp = a.groups[gi];
   // workgroup-uniform: kept in scalar registers (they form the scalar offsets of the operand loads)
   const int so = __builtin_amdgcn_readfirstlane(grp.x), b0 = __builtin_amdgcn_readfirstlane(grp.y),
@@ -50,9 +60,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int lr = lane & 31, h = lane >> 5;
   const int bi = w >> 1, hp = w & 1;
-  const int r0 = chunk * a.chunk_rows;
-  const int r1 = min(a.B, r0 + a.chunk_rows);
-  const bool writer = DBB && a.dz_out && grp.w;
+  // the groups of an output slab all rebuild the same dz: item i is stored by the
+  // group of rank i % count, so the stores are spread evenly over them
+  const int wrank = __builtin_amdgcn_readfirstlane(grp.w) & 255, wcount = __builtin_amdgcn_readfirstlane(grp.w) >> 8;
+  const bool may_write = DBB && a.dz_out != nullptr;
+  const int R = pl.item_rows, istride = pl.stride;
 
   {
     const int c = t & 63, k = t >> 6;  // 4 x 64 entries per pass
@@ -88,22 +100,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   const int tile0 = 0;
 #else
 #define DW_TILE(BASE) ((BASE) / kRT)
-  const int tile0 = r0 / kRT;
+  const int tile0 = 0;
 #endif
   // Operand loads are buffer loads (gemm_bs.hip): one resource per operand over
-  // this chunk's row tiles, the (tile, slab) part of the address in scalar
-  // registers, this thread's two float4 slots as constant lane offsets.
+  // all its row tiles (< 4 GB: checked by the launcher), the (tile, slab) part
+  // of the address in scalar registers, this thread's two float4 slots as
+  // constant lane offsets.
 #ifdef EXP_DW_HOT
   const int ntile = 4;
 #else
-  const int ntile = max(0, (r1 - r0 + kRT - 1) / kRT);
+  const int ntile = (a.B + kRT - 1) / kRT;
 #endif
   const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((const char*)a.A + (size_t)tile0 * S_a * 8192), 0, ntile * S_a * 8192, 0x00020000);
+      (void*)((const char*)a.A + (size_t)tile0 * S_a * 8192), 0, (unsigned)ntile * S_a * 8192u, 0x00020000);
   const __amdgpu_buffer_rsrc_t dres = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((const char*)a.D + (size_t)tile0 * S_d * 8192), 0, ntile * S_d * 8192, 0x00020000);
+      (void*)((const char*)a.D + (size_t)tile0 * S_d * 8192), 0, (unsigned)ntile * S_d * 8192u, 0x00020000);
   const __amdgpu_buffer_rsrc_t zres = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((const char*)(DBB ? a.d_z : a.D) + (size_t)tile0 * S_d * 8192), 0, ntile * S_d * 8192, 0x00020000);
+      (void*)((const char*)(DBB ? a.d_z : a.D) + (size_t)tile0 * S_d * 8192), 0, (unsigned)ntile * S_d * 8192u, 0x00020000);
   typedef float v4f_t __attribute__((ext_vector_type(4)));
 #define DW_BUFLD(RES, VOFF, SOFF)                                                      \
   ({                                                                                   \
@@ -114,11 +127,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
 #define DW_GLOAD(BASE)                                                     \
   {                                                                        \
     const int t_ = DW_TILE(BASE) - tile0;                                  \
-    const int oa0 = (t_ * S_a + si0) * 8192, od = (t_ * S_d + so) * 8192;  \
+    const int oa0 = (int)((unsigned)(t_ * S_a + si0) * 8192u), od = (int)((unsigned)(t_ * S_d + so) * 8192u); \
     ra0 = DW_BUFLD(ares, v40, oa0);                                        \
     ra1 = DW_BUFLD(ares, v41, oa0);                                        \
     if (two) {                                                             \
-      const int oa1 = (t_ * S_a + si1) * 8192;                             \
+      const int oa1 = (int)((unsigned)(t_ * S_a + si1) * 8192u);           \
       rb0 = DW_BUFLD(ares, v40, oa1);                                      \
       rb1 = DW_BUFLD(ares, v41, oa1);                                      \
     }                                                                      \
@@ -129,10 +142,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
       rz1 = DW_BUFLD(zres, v41, od);                                       \
     }                                                                      \
   }
-  if (r0 < r1) DW_GLOAD(r0);
-  for (int base = r0; base < r1; base += kRT) {
+  // stages of this workgroup: its items, 32 rows a stage; the next stage's rows
+  // are known one stage ahead (its loads go out early)
+  int it = 0, item = item0, base = item0 * R, iend = min(a.B, base + R);
+  bool more = n_it > 0 && base < a.B;
+  if (more) DW_GLOAD(base);
+  while (more) {
+    int nbase = base + kRT, nit = it, nitem = item, nend = iend;
+    if (nbase >= iend) {
+      nit = it + 1;
+      nitem = item + istride;
+      nbase = nitem * R;
+      nend = min(a.B, nbase + R);
+    }
+    const bool nmore = nit < n_it && nbase < a.B;
+    const int r1 = iend;
+    const bool writer = may_write && item % wcount == wrank;
+#ifndef EXP_DW_NOBAR1
     __syncthreads();  // previous stage's fragment reads are done (and the tables written)
+#endif
     const bool v0 = base + sr < r1, v1 = base + sr + 16 < r1;
+#ifndef EXP_DW_NOSTAGE  // diagnostic build without the staging phase (loads, transforms, scatter)
     if constexpr (PRO) {
       const float4 sc0 = *(const float4*)(tab + f0), sh0 = *(const float4*)(tab + 64 + f0);
       ra0 = bnact4(ra0, sc0, sh0, a.alpha);
@@ -187,21 +217,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
       DW_PUT(Ds, rd0, o0) DW_PUT(Ds, rd1, o1)
 #undef DW_PUT
     }
+#endif
     // the next stage's loads go out before the barrier (its wait hides part of
     // their latency; 976 -> 914 us measured), and the MFMA phase runs at raised
     // wave priority so the other waves' staging does not starve it
-    if (base + kRT < r1) DW_GLOAD(base + kRT);
+    if (nmore) DW_GLOAD(nbase);
+#ifndef EXP_DW_NOBAR2
     __syncthreads();
+#endif
+#if defined(EXP_DW_ROTPRIO)  // diagnostic: the priority of the MFMA phase rotates with the item, offset by dispatch layer
+    switch (((blockIdx.x >> 8) + it) & 3) {
+      case 0: __builtin_amdgcn_s_setprio(0); break;
+      case 1: __builtin_amdgcn_s_setprio(1); break;
+      case 2: __builtin_amdgcn_s_setprio(2); break;
+      default: __builtin_amdgcn_s_setprio(3); break;
+    }
+#elif defined(EXP_DW_NOPRIO)   // diagnostic builds: no raised priority / a different level per workgroup
+#elif defined(EXP_DW_PRIOWG)
+    switch (blockIdx.x % 3) {
+      case 0: __builtin_amdgcn_s_setprio(1); break;
+      case 1: __builtin_amdgcn_s_setprio(2); break;
+      default: __builtin_amdgcn_s_setprio(3); break;
+    }
+#else
     __builtin_amdgcn_s_setprio(1);
+#endif
+#ifndef EXP_DW_NOMFMA  // diagnostic build without the fragment reads and MFMAs
     if (two) {
       const float* Ap = As[bi] + (32 * hp + lr) * kDwLd + 4 * h;
       const float* D0 = Ds + lr * kDwLd + 4 * h;
       const float* D1 = Ds + (32 + lr) * kDwLd + 4 * h;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const float4 av = *(const float4*)(Ap + 8 * g);
-        const float4 d0 = *(const float4*)(D0 + 8 * g);
-        const float4 d1 = *(const float4*)(D1 + 8 * g);
+#ifdef EXP_DW_FEWREADS  // diagnostic: one fragment set per stage instead of four
+        const int go = 0;
+#else
+        const int go = 8 * g;
+#endif
+        const float4 av = *(const float4*)(Ap + go);
+        const float4 d0 = *(const float4*)(D0 + go);
+        const float4 d1 = *(const float4*)(D1 + go);
         acc0 = MFMA32(av.x, d0.x, acc0);
         acc1 = MFMA32(av.x, d1.x, acc1);
         acc0 = MFMA32(av.y, d0.y, acc0);
@@ -224,14 +279,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
         acc0 = MFMA32(av.w, dv.w, acc0);
       }
     }
+#endif
     __builtin_amdgcn_s_setprio(0);
+    base = nbase;
+    it = nit;
+    item = nitem;
+    iend = nend;
+    more = nmore;
   }
 #undef DW_GLOAD
 #undef DW_BUFLD
 #undef DW_TILE
 #undef DW_IX
+#ifdef EXP_CLOCK
+  if (threadIdx.x == 0 && a.clk) {
+    const uint64_t ck1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    a.clk[4 * blockIdx.x] = ck1 - ck0;
+    a.clk[4 * blockIdx.x + 1] = rt1 - rt0;
+    a.clk[4 * blockIdx.x + 2] = rt0;
+    a.clk[4 * blockIdx.x + 3] = rt1;
+  }
+#endif
+  // this slot's partial of each block
   if (two) {
-    float* out = a.part + ((size_t)chunk * a.nblk + (bi ? b1 : b0)) * 4096;
+    float* out = a.part + ((size_t)slot * a.nblk + (bi ? b1 : b0)) * 4096;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int p = 32 * hp + (k & 3) + 8 * (k >> 2) + 4 * h;
@@ -239,7 +310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
       out[p * 64 + 32 + lr] = acc1[k];
     }
   } else {
-    float* out = a.part + ((size_t)chunk * a.nblk + b0) * 4096 + 32 * bi;
+    float* out = a.part + ((size_t)slot * a.nblk + b0) * 4096 + 32 * bi;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int p = 32 * hp + (k & 3) + 8 * (k >> 2) + 4 * h;
@@ -248,8 +319,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   }
 }
 
+int gemm_dw_resident_slots() {
+  // the instance the training step runs most (BN-apply A x BN-backward D); the
+  // others need no more registers or LDS
+  int dev = 0, per_cu = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm_dw_kernel<true, true, false>, 256, 0) != hipSuccess)
+    return 0;
+  return per_cu * prop.multiProcessorCount;
+}
+
 void launch_gemm_dw(const GemmDwArgs& a, hipStream_t s) {
-  const int grid = a.ngroups * a.nchunks;
+  const int grid = a.n_wg;
   const bool pro = a.pro_scale != nullptr, dbb = a.d_bnback != 0;
   // the dropout variants are separate instances: the mask hash costs registers
   const bool drop = dbb && a.d_drop.rate > 0.f;

@@ -101,8 +101,13 @@ struct Handle {
   // DZ: dz of a hidden layer, stored by its weight-gradient GEMM
   float *DH = nullptr, *DG = nullptr, *DZ = nullptr;
   // weight-gradient work groups (kernels_gemm.hip): up to 2 blocks sharing an output slab
-  int4 *grp_hidden = nullptr, *grp_lift = nullptr, *grp_out = nullptr;
-  int ngrp_hidden = 0, ngrp_lift = 0, ngrp_out = 0;
+  struct DwMap { int64_t B; DwPlan plan; int4* dev; int n; };   // workgroup map of a launch (make_dw_wgmap)
+  struct DwGroups {
+    int4* dev = nullptr; int n = 0;
+    std::vector<DwMap> maps;     // made on first use per batch size
+  };
+  DwGroups grp_hidden, grp_lift, grp_out;
+  int dw_slots = 0;               // weight-gradient workgroups the GPU holds at once
 
   std::vector<BnStats> bn;
   std::vector<double*> zsum;      // per BN layer: column sums of z (bias-gradient term)
@@ -113,6 +118,7 @@ struct Handle {
   int small_rt = 0;               // launches of at most this many row tiles use the small-batch GEMM
   double2* colacc = nullptr;      // [kColSplit][H] float64 column sums
   float* dw_part = nullptr;
+  size_t dw_cap = 0;              // floats in dw_part (sized for max_batch)
   double *loss_part = nullptr, *loss_sum = nullptr, *acc1 = nullptr, *acc2 = nullptr;
   double* db_part = nullptr;      // [loss_grid][64] column sums of dy per out_assemble workgroup
   int loss_grid = 1;
@@ -164,6 +170,7 @@ struct Handle {
   // batches are launch-bound (fit's reference batch is 200)
   struct StepGraph { int64_t B; bool update, keep; hipGraphExec_t exec; };
   std::vector<StepGraph> graphs;
+  bool capturing = false;  // a step graph is being captured (no allocation / blocking copy allowed)
   int use_graphs = 0;  // LCN_GRAPHS=1 turns them on (rocprofv3 kernel tracing crashed on graph launches)
   float* lr_dev = nullptr;  // Adam's lr_t of the running step
   Timer timers[LCN_K_NUM];
@@ -227,8 +234,10 @@ int upload(Handle* h, T** p, const std::vector<T>& src) {
 int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Pair the blocks of each output slab into weight-gradient work groups
-// (so, block0, block1 | -1, stores dz): the first group of a slab stores dz.
-int upload_dw_groups(Handle* h, const std::vector<int2>& blk, int4** dev, int* n) {
+// (so, block0, block1 | -1, rank | count << 8): the group's rank among the
+// groups of its output slab and their number -- they all rebuild the same dz
+// and take turns storing it (item i is stored by the group of rank i % count).
+int upload_dw_groups(Handle* h, const std::vector<int2>& blk, Handle::DwGroups* out) {
   int nso = 0;
   for (const int2& b : blk) nso = std::max(nso, b.y + 1);
   std::vector<int4> g;
@@ -237,10 +246,10 @@ int upload_dw_groups(Handle* h, const std::vector<int2>& blk, int4** dev, int* n
     for (size_t b = 0; b < blk.size(); ++b)
       if (blk[b].y == so) ids.push_back((int)b);
     for (size_t i = 0; i < ids.size(); i += 2)
-      g.push_back(make_int4(so, ids[i], i + 1 < ids.size() ? ids[i + 1] : -1, i == 0 ? 1 : 0));
+      g.push_back(make_int4(so, ids[i], i + 1 < ids.size() ? ids[i + 1] : -1, (int)(i / 2) | ((int)((ids.size() + 1) / 2) << 8)));
   }
-  *n = (int)g.size();
-  return upload(h, dev, g);
+  out->n = (int)g.size();
+  return upload(h, &out->dev, g);
 }
 
 // batch chunks of a weight-gradient launch (partials per block = chunks);
@@ -256,6 +265,16 @@ int dw_chunks(int nblk, int64_t B) {
   static const int lo = std::getenv("LCN_DW_MINCH") ? std::atoi(std::getenv("LCN_DW_MINCH")) : 16;
   const int by_rows = (int)std::min<int64_t>(cap, B / 2048);
   return std::max(std::max(lo, by_rows), std::min(cap, budget / std::max(1, nblk)));
+}
+
+// How a weight-gradient launch over the groups g (nblk blocks) splits B rows
+// (lcn_internal.h DwPlan): XCD-strided items in rounds of falling size when
+// the groups are few, dw_chunks contiguous chunks otherwise; at most 128
+// partials a block.  LCN_DW_SLOTS overrides the resident-slot count (0: always
+// contiguous chunks).
+DwPlan dw_plan(const Handle* h, const Handle::DwGroups& g, int nblk, int64_t B) {
+  static const int slots_env = std::getenv("LCN_DW_SLOTS") ? std::atoi(std::getenv("LCN_DW_SLOTS")) : -1;
+  return make_dw_plan(B, g.n, slots_env >= 0 ? slots_env : h->dw_slots, dw_chunks(nblk, B), 128);
 }
 
 // Launches of at most this many 32-row tiles run the small-batch kernel, which
@@ -366,7 +385,7 @@ int build(Handle* h, const lcn_config* c) {
     bptr.push_back((int)bidx.size());
   }
   CHECK(upload(h, &h->blk, blk));
-  CHECK(upload_dw_groups(h, blk, &h->grp_hidden, &h->ngrp_hidden));
+  CHECK(upload_dw_groups(h, blk, &h->grp_hidden));
   CHECK(upload(h, &h->fwd_ptr, fptr));
   CHECK(upload(h, &h->bwd_ptr, bptr));
   CHECK(upload(h, &h->fwd_idx, fidx));
@@ -404,8 +423,8 @@ int build(Handle* h, const lcn_config* c) {
   CHECK(upload(h, &h->out_idx, oidx));
   CHECK(upload(h, &h->lift_blk, lblk));
   CHECK(upload(h, &h->out_blk, oblk));
-  CHECK(upload_dw_groups(h, lblk, &h->grp_lift, &h->ngrp_lift));
-  CHECK(upload_dw_groups(h, oblk, &h->grp_out, &h->ngrp_out));
+  CHECK(upload_dw_groups(h, lblk, &h->grp_lift));
+  CHECK(upload_dw_groups(h, oblk, &h->grp_out));
 
   // ---- per-layer weight forms ----
   for (int k = 0; k < nl; ++k) {
@@ -541,10 +560,12 @@ int build(Handle* h, const lcn_config* c) {
   // holds at least 64 rows): 16 KB per block and chunk -- 92 MB at the cfg3
   // shape (175 blocks, 32 chunks), 1.2 GB at the cfg4 shape with 16 384 rows
   // (4 624 blocks, 16 chunks)
-  auto launch_chunks = [&](int nb) { return std::max<int64_t>(1, std::min<int64_t>(dw_chunks(nb, B), cdiv(B, 64))); };
-  const size_t dw_elems = (size_t)std::max(launch_chunks(h->nblk) * h->nblk,
-                                           launch_chunks(h->nslab) * h->nslab) * 4096;
-  CHECK(dalloc(h, &h->dw_part, dw_elems));
+  h->dw_slots = gemm_dw_resident_slots();
+  if (h->dw_slots <= 0) { h->err = "occupancy query of the weight-gradient kernel failed"; return LCN_E_HIP; }
+  h->dw_cap = (size_t)std::max({(int64_t)dw_plan_slots(dw_plan(h, h->grp_hidden, h->nblk, B)) * h->nblk,
+                                (int64_t)dw_plan_slots(dw_plan(h, h->grp_lift, h->nslab, B)) * h->nslab,
+                                (int64_t)dw_plan_slots(dw_plan(h, h->grp_out, h->nslab, B)) * h->nslab}) * 4096;
+  CHECK(dalloc(h, &h->dw_part, h->dw_cap));
   return LCN_OK;
 }
 
@@ -797,6 +818,36 @@ int gemm_hidden(Handle* h, int k, int kindt, const Operand& X, float* Y, const f
   return gemm(h, c, B);
 }
 
+// the workgroup map of a launch (make_dw_wgmap), uploaded once per batch size
+int dw_map(Handle* h, Handle::DwGroups* g, const DwPlan& plan, int64_t B, const Handle::DwMap** out) {
+  for (const auto& e : g->maps)
+    if (e.B == B && e.plan.item_rows == plan.item_rows && e.plan.stride == plan.stride &&
+        e.plan.n_slots == plan.n_slots && e.plan.sub == plan.sub) { *out = &e; return LCN_OK; }
+  if (h->capturing) { h->err = "internal: weight-gradient map missing during graph capture"; return LCN_E_STATE; }
+  if (g->maps.size() >= 64) {  // many batch sizes on one handle: start over (the maps are small)
+    HIPC(hipStreamSynchronize(h->stream));
+    for (auto& e : g->maps) {
+      hipFree(e.dev);
+      h->allocs.erase(std::find(h->allocs.begin(), h->allocs.end(), (void*)e.dev));
+    }
+    g->maps.clear();
+  }
+  const std::vector<int4> map = make_dw_wgmap(g->n, plan, B);
+  int4* dev = nullptr;
+  CHECK(upload(h, &dev, map));
+  g->maps.push_back(Handle::DwMap{B, plan, dev, (int)map.size()});
+  *out = &g->maps.back();
+  return LCN_OK;
+}
+// every map a step at batch B launches with (before a graph capture)
+int dw_maps_ready(Handle* h, int64_t B) {
+  const Handle::DwMap* m = nullptr;
+  CHECK(dw_map(h, &h->grp_hidden, dw_plan(h, h->grp_hidden, h->nblk, B), B, &m));
+  CHECK(dw_map(h, &h->grp_lift, dw_plan(h, h->grp_lift, h->nslab, B), B, &m));
+  CHECK(dw_map(h, &h->grp_out, dw_plan(h, h->grp_out, h->nslab, B), B, &m));
+  return LCN_OK;
+}
+
 // dW_e of a layer from A (input activations, raw or BN-apply prologue) and D
 // (raw, or dz rebuilt from (dh, z) by the BN backward prologue -- then also
 // stored to dz_out when given): partial slabs per batch chunk, then a
@@ -829,21 +880,33 @@ int gemm_dw(Handle* h, const Operand& A, const Operand& D, const int2* blk, int 
   a.alpha = h->alpha;
   a.blk = blk;
   a.nblk = nblk;
-  if (blk == h->blk) { a.groups = h->grp_hidden; a.ngroups = h->ngrp_hidden; }
-  else if (blk == h->lift_blk) { a.groups = h->grp_lift; a.ngroups = h->ngrp_lift; }
-  else if (blk == h->out_blk) { a.groups = h->grp_out; a.ngroups = h->ngrp_out; }
-  else { h->err = "internal: unknown block list"; return LCN_E_ARG; }
+  Handle::DwGroups* g = blk == h->blk ? &h->grp_hidden : blk == h->lift_blk ? &h->grp_lift
+                        : blk == h->out_blk ? &h->grp_out : nullptr;
+  if (!g) { h->err = "internal: unknown block list"; return LCN_E_ARG; }
+  a.groups = g->dev;
+  a.ngroups = g->n;
   a.B = B;
-  const int nch = std::max(1, std::min<int>(dw_chunks(nblk, B), (int)cdiv(B, 64)));
-  a.chunk_rows = (int)(cdiv(cdiv(B, nch), 64) * 64);
-  a.nchunks = (int)cdiv(B, a.chunk_rows);
+  a.plan = dw_plan(h, *g, nblk, B);
+  if ((size_t)dw_plan_slots(a.plan) * nblk * 4096 > h->dw_cap) {
+    h->err = "internal: weight-gradient partials exceed their buffer";
+    return LCN_E_STATE;
+  }
+  const Handle::DwMap* m = nullptr;
+  CHECK(dw_map(h, g, a.plan, B, &m));
+  a.wgmap = m->dev;
+  a.n_wg = m->n;
+  // the kernel addresses its operands with 32-bit byte offsets
+  if ((uint64_t)tiled_floats(B, std::max(A.S, D.S)) * 4 >= (1ull << 32)) {
+    h->err = "batch too large for the weight-gradient kernel (an operand of 4 GB or more)";
+    return LCN_E_ARG;
+  }
   a.part = h->dw_part;
   hipEvent_t ev[2];
   if (timer >= 0) tstart(h, timer, ev);
   launch_gemm_dw(a, h->stream);
   if (timer >= 0)
     tstop(h, timer, ev, timer == LCN_K_GEMM_DW ? 2.0 * 4096.0 * nblk * B : 4.0 * (h->H + 51) * (double)B);
-  launch_dw_reduce(h->dw_part, a.nchunks, nblk, blk, dW, ld, rows_valid, cols_valid, h->stream);
+  launch_dw_reduce(h->dw_part, dw_plan_slots(a.plan), nblk, blk, dW, ld, rows_valid, cols_valid, h->stream);
   return LCN_OK;
 }
 
@@ -1254,8 +1317,11 @@ static int step_graph(Handle* h, int64_t B, bool update, bool keep, hipGraphExec
   for (const auto& g : h->graphs)
     if (g.B == B && g.update == update && g.keep == keep) { *out = g.exec; return LCN_OK; }
   hipGraph_t graph = nullptr;
+  CHECK(dw_maps_ready(h, B));
   HIPC(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
+  h->capturing = true;
   const int rc = enqueue_step(h, B, update, keep);
+  h->capturing = false;
   const hipError_t ec = hipStreamEndCapture(h->stream, &graph);
   if (rc != LCN_OK) { if (graph) hipGraphDestroy(graph); return rc; }
   if (ec != hipSuccess) { h->err = std::string("step graph capture: ") + hipGetErrorString(ec); return LCN_E_HIP; }

@@ -4,7 +4,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
+#include <vector>
 
 namespace lcn {
 
@@ -135,9 +137,96 @@ void launch_gemm_bs(const GemmArgs& a, hipStream_t s);
 // 32-row tile (not per 128-row group); no dropout epilogue
 void launch_gemm_bs_small(const GemmArgs& a, hipStream_t s);
 
+// How a weight-gradient launch splits the batch (kernels_gemm.hip).  The batch
+// is cut into items of item_rows rows (a multiple of 32).  A workgroup is
+// (group of blocks, partial slot, first item, item count): it walks its items
+// first, first + stride, ... and keeps its accumulators over all of them, then
+// writes one partial slab per block into its slot; a block has n_slots
+// partials (every slot of every group is written, so dw_reduce sums them all).
+//  * few groups (cfg3: 93; make_dw_plan picks stride 8): item i belongs to XCD
+//    i % 8 -- every workgroup of XCD x (workgroups b, b + 8, ... share an XCD
+//    and its L2) walks items = x (mod 8), so the groups that read the same rows
+//    at the same time share them through that L2.  An XCD's items are dealt in
+//    rounds of falling size (1/2, 1/4, 1/8, 1/8 of them): one workgroup per
+//    group and round, dispatched round by round, so the launch ends with short
+//    workgroups.  With 32 equal contiguous chunks a launch was ~3 rounds of
+//    ~170 us workgroups and its last 15 % ran at ~35 % residency.  Very few
+//    groups (the thin layers: 9 / 17): a round's items of an XCD are further
+//    cut into `sub` parts so the launch still has ~3 x the resident workgroups.
+//  * many groups (the cfg4 shape: 2 312; stride 1): n_slots contiguous chunks
+//    per group, one item each (item_rows = rows per chunk), tens of rounds.
+struct DwPlan { int item_rows, stride, n_slots, sub; };
+inline int dw_plan_slots(const DwPlan& p) { return p.n_slots; }
+constexpr int kDwRounds = 4;
+// groups: number of block groups; slots: workgroups the GPU holds at once;
+// chunks: the contiguous-chunk count of the many-groups case; max_slots: cap on
+// the partials per block
+inline DwPlan make_dw_plan(int64_t B, int groups, int slots, int chunks, int max_slots) {
+  DwPlan p{};
+  const int64_t n64 = (B + 63) / 64;
+  if (groups * 8 <= slots && 8 * kDwRounds <= max_slots) {
+    // >= 64 items per XCD where the batch allows (16 for the shortest round), at most 256 rows an item
+    const int64_t r = B / (8 * 64);
+    p.item_rows = (int)std::min<int64_t>(256, std::max<int64_t>(64, r / 64 * 64));
+    p.stride = 8;
+    const int64_t per_xcd = ((B + p.item_rows - 1) / p.item_rows + 7) / 8;
+    const int rounds = (int)std::max<int64_t>(1, std::min<int64_t>(kDwRounds, per_xcd / 4));
+    // ~3 x the resident workgroups in all, within the partial cap and >= 2 items a workgroup
+    int sub = std::max(1, (3 * slots - 96 + groups * 8 * rounds - 1) / (groups * 8 * rounds));
+    sub = (int)std::min<int64_t>({(int64_t)sub, (int64_t)max_slots / (8 * rounds), std::max<int64_t>(1, per_xcd / (2 * rounds))});
+    p.sub = std::max(1, sub);
+    p.n_slots = 8 * rounds * p.sub;
+    return p;
+  }
+  const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(std::min(chunks, max_slots), n64));
+  p.item_rows = (int)(((B + nch - 1) / nch + 63) / 64 * 64);
+  p.stride = 1;
+  p.sub = 1;
+  p.n_slots = (int)((B + p.item_rows - 1) / p.item_rows);
+  return p;
+}
+// The workgroups of a launch: entry b is workgroup blockIdx.x = b as (group,
+// slot, first item, item count); (-1, 0, 0, 0) pads the XCD lists to equal
+// length.  Stride 8: entry 8 i + x is the i-th workgroup of XCD x, rounds in
+// order, groups in order within a round; a round's share of the n items of the
+// XCD: n/2, n/4, ..., the last round takes the rest.
+inline std::vector<int4> make_dw_wgmap(int groups, const DwPlan& p, int64_t B) {
+  const int n_items = (int)((B + p.item_rows - 1) / p.item_rows);
+  if (p.stride == 1) {
+    std::vector<int4> map;
+    for (int c = 0; c < p.n_slots; ++c)
+      for (int g = 0; g < groups; ++g) map.push_back(make_int4(g, c, c, c < n_items ? 1 : 0));
+    // chunk-major: the groups of a chunk are adjacent; give each XCD whole chunks
+    // (a contiguous range of entries) by interleaving the ranges
+    const int n = (int)map.size(), q = n >> 3, r = n & 7;
+    std::vector<int4> out(8 * ((n + 7) / 8), make_int4(-1, 0, 0, 0));
+    for (int x = 0; x < 8; ++x) {
+      const int lo = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q, cnt = q + (x < r ? 1 : 0);
+      for (int i = 0; i < cnt; ++i) out[8 * i + x] = map[lo + i];
+    }
+    return out;
+  }
+  const int sub = std::max(1, p.sub), rounds = p.n_slots / (8 * sub);
+  std::vector<int4> map((size_t)8 * rounds * sub * groups, make_int4(-1, 0, 0, 0));
+  for (int x = 0; x < 8; ++x) {
+    const int n = n_items > x ? (n_items - x + 7) / 8 : 0;  // items x, x + 8, ... of this XCD
+    int a = 0;
+    for (int r = 0; r < rounds; ++r) {
+      const int cnt = r + 1 < rounds ? (n - a + 1) / 2 : n - a;
+      for (int u = 0; u < sub; ++u) {  // the round's items in `sub` contiguous parts
+        const int lo = a + (int)((int64_t)cnt * u / sub), hi = a + (int)((int64_t)cnt * (u + 1) / sub);
+        for (int g = 0; g < groups; ++g)
+          map[8 * (((size_t)r * sub + u) * groups + g) + x] = make_int4(g, 8 * (r * sub + u) + x, x + 8 * lo, hi - lo);
+      }
+      a += cnt;
+    }
+  }
+  return map;
+}
 // dWe blocks: part[chunk][blk][p][q] = sum_{b in chunk} A[b, si*64+p] * D[b, so*64+q]
 // Work unit = a group of up to 2 blocks with the same output slab so (they
-// share the staged D operand): int4 (so, block0, block1 or -1, stores dz).
+// share the staged D operand): int4 (so, block0, block1 or -1, rank | count << 8
+// of the group among the groups of so, which take turns storing dz).
 struct GemmDwArgs {
   const float* A; int S_a;           // tiled
   const float* D; int S_d;           // tiled; d_bnback: D = dh and the operand is dz
@@ -149,10 +238,16 @@ struct GemmDwArgs {
   const int2* blk;                   // (si, so) per block
   int nblk;
   const int4* groups; int ngroups;   // block groups (see above)
-  int B; int chunk_rows; int nchunks;  // chunk_rows: multiple of 64
-  float* part;                       // [nchunks][nblk][4096]
+  int B; DwPlan plan;                // how the batch is split (see DwPlan)
+  const int4* wgmap; int n_wg;       // the launch's workgroups (make_dw_wgmap)
+  float* part;                       // [dw_plan_slots(plan)][nblk][4096]
+#ifdef EXP_CLOCK
+  uint64_t* clk;                     // diagnostic build: per workgroup (shader clocks, 100 MHz ticks, start, end)
+#endif
 };
 void launch_gemm_dw(const GemmDwArgs& a, hipStream_t s);
+// workgroups of the weight-gradient kernel the current device holds at once
+int gemm_dw_resident_slots();
 // sum partials over chunks; write into dense dW [rows][ld] at (si*64+p, so*64+q),
 // dropping rows >= rows_valid / columns >= cols_valid (padding of thin layers)
 void launch_dw_reduce(const float* part, int nchunks, int nblk, const int2* blk,
