@@ -85,10 +85,15 @@ typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
   __builtin_amdgcn_raw_ptr_buffer_load_lds(wres, (__attribute__((address_space(3))) void*)(DST), 16, xlo, (SOFF), 0, 0);
 #define LOADW(BLK, BUF)                                                   \
   {                                                                       \
-    const int bo_ = (BLK) * 16384 + wv_u * 1024;  /* this wave's 1 KB of each 4 KB quarter */ \
+    const int bo_ = (BLK) * 16384 + wv_u * 1024;  /* this wave's 1 KB of each 4 KB quarter (8 KB half) */ \
     float4* d_ = Wl + (BUF) * 1024 + (threadIdx.x & ~63);                 \
-    GLDS(bo_, d_) GLDS(bo_ + 4096, d_ + 256) GLDS(bo_ + 8192, d_ + 512)   \
-    if constexpr (KG > 6) GLDS(bo_ + 12288, d_ + 768)                     \
+    if constexpr (kGemmWaves == 8) {                                      \
+      GLDS(bo_, d_)                                                       \
+      if (KG > 7 || wv_u + 8 < 2 * KG) GLDS(bo_ + 8192, d_ + 512)         \
+    } else {                                                              \
+      GLDS(bo_, d_) GLDS(bo_ + 4096, d_ + 256) GLDS(bo_ + 8192, d_ + 512) \
+      if constexpr (KG > 6) GLDS(bo_ + 12288, d_ + 768)                   \
+    }                                                                     \
   }
 // BN apply + LeakyReLU of one activation fragment (k-group G of a slab whose
 // first channel is CH), scale / shift from the LDS tables
@@ -135,8 +140,12 @@ constexpr int kEpiBnBackDrop = 3;
 // the hidden layers; the lift's input slab holds 17 * in_F = 34 or 51 features
 // and zeros (its weight rows there are zero too), so its instances stop after
 // 5 or 7 groups: the thin layer is MFMA-bound at the padded width.
+// float4 offset of the BN tables / epilogue constants / wave merge in LDS: after
+// the weight double buffer (2 x 16 KB) and the epilogue's 8 KB per wave
+constexpr int kTabOff = kGemmWaves > 4 ? kGemmWaves * 512 : 2048;
+
 template <int PRO, int EPI, int KG = 8>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gemm_bs_kernel(GemmArgs a) {
+__global__ __launch_bounds__(64 * kGemmWaves) __attribute__((amdgpu_waves_per_eu(4))) void gemm_bs_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) float4 Wl[];  // [2][1024] (+ BN tables)
 #ifdef EXP_CLOCK
   // diagnostic build: shader-clock and 100 MHz real-time stamps around the
@@ -227,8 +236,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
     for (int q = 0; q < 8; ++q) rq[q] = zero4;
   }
   if constexpr (PRO == PRO_BNACT) {  // BN scale / shift of the operand's layer -> LDS
-    float* tb = (float*)(Wl + 2048);
-    for (int c = threadIdx.x; c < a.pro_F; c += 256) {
+    float* tb = (float*)(Wl + kTabOff);
+    for (int c = threadIdx.x; c < a.pro_F; c += 64 * kGemmWaves) {
       tb[c] = a.pro_scale[c];
       tb[a.pro_F + c] = a.pro_shift[c];
     }
@@ -238,11 +247,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   // EPI_BNBACK reads z of the layer below after the loop; the per-channel BN
   // constants of this output slab go to an LDS table
   float4 zp0, zp1, zp2, zp3, zp4, zp5, zp6, zp7;
-  float* ptab = (float*)(Wl + 2048);  // [4][64]: scale, shift, mean, rstd
+  float* ptab = (float*)(Wl + kTabOff);  // [4][64]: scale, shift, mean, rstd
   if constexpr (EPI == EPI_BNBACK || EPI == kEpiBnBackDrop) {
     const int pk = threadIdx.x >> 6, ch = (so % (a.epi_F / kSlab)) * kSlab + lane;
     const float* src = pk == 0 ? a.epi_scale : pk == 1 ? a.epi_shift : pk == 2 ? a.epi_mean : a.epi_rstd;
-    ptab[threadIdx.x] = src[ch];
+    if (pk < 4) ptab[threadIdx.x] = src[ch];
   }
   f32x16 acc0, acc1;
 #pragma unroll
@@ -326,7 +335,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   const int c = lane, cg = c >> 3, chh = (c >> 2) & 1, cs = c & 3;
   const int n = live ? min(kRT, a.B - rt * kRT) : 0;  // valid rows of the tile
   // the 4 waves' column partials are merged into one per 128-row group
-  float* comb = (float*)(Wl + 2048) + 256;  // [4 waves][64 columns][3]
+  float* comb = (float*)(Wl + kTabOff) + 256;  // [waves][64 columns][3]
   float2* stat = a.stat + (size_t)rtg * ncols + so * kSlab + c;
   auto put = [&](int q, float x0, float x1, float x2, float x3) {
     const int pos = lane ^ (2 * q + h);
@@ -472,10 +481,11 @@ void launch_gemm_bs(const GemmArgs& a, hipStream_t s) {
   const int grid = 8 * ((n_rtg + 7) / 8) * a.n_out_slabs;  // 8 XCDs x row-tile groups per XCD x slabs
   // weight double buffer; BN tables / epilogue constants and the 4-wave merge after it
   const size_t lds = 2 * 1024 * sizeof(float4);
-  const size_t ldse = lds + (256 + 4 * 64 * 3) * sizeof(float);
-  const size_t ldsp = std::max(lds + 2 * a.pro_F * sizeof(float), ldse);
-#define LAUNCH(P, E, L) hipLaunchKernelGGL((gemm_bs_kernel<P, E>), dim3(grid), dim3(256), L, s, a)
-#define LAUNCHK(P, E, K, L) hipLaunchKernelGGL((gemm_bs_kernel<P, E, K>), dim3(grid), dim3(256), L, s, a)
+  const size_t tab = kTabOff * sizeof(float4);
+  const size_t ldse = tab + (256 + kGemmWaves * 64 * 3) * sizeof(float);
+  const size_t ldsp = std::max(tab + 2 * a.pro_F * sizeof(float), ldse);
+#define LAUNCH(P, E, L) hipLaunchKernelGGL((gemm_bs_kernel<P, E>), dim3(grid), dim3(64 * kGemmWaves), L, s, a)
+#define LAUNCHK(P, E, K, L) hipLaunchKernelGGL((gemm_bs_kernel<P, E, K>), dim3(grid), dim3(64 * kGemmWaves), L, s, a)
   if (a.k_groups == 5 || a.k_groups == 7) {  // the lift: raw operand, BN statistics or none
     const bool k5 = a.k_groups == 5;
     if (a.epi_mode == EPI_BNFWD) { if (k5) LAUNCHK(PRO_RAW, EPI_BNFWD, 5, ldse); else LAUNCHK(PRO_RAW, EPI_BNFWD, 7, ldse); }

@@ -13,7 +13,11 @@ namespace lcn {
 constexpr int kJ = 17;          // joints (models_att.py:512-513)
 constexpr int kSlab = 64;       // feature slab = MFMA tile edge; F is a multiple of it
 constexpr int kRT = 32;         // rows per row tile of the activation layout
+#ifdef EXP_GEMM_WAVES8  // diagnostic build: 8 row tiles per workgroup (half the weight LDS-DMA per wave)
+constexpr int kGemmWaves = 8;
+#else
 constexpr int kGemmWaves = 4;   // row tiles (one per wave) per block-sparse GEMM workgroup
+#endif
 constexpr int kGemmRows = kRT * kGemmWaves;  // rows per workgroup = per BN partial
 
 // ----------------------------------------------------------------------------

@@ -181,3 +181,36 @@ def test_tta_predict_matches_inference_pipeline(flags):
     # the 2x2 product) moves that pose's prediction by float32 rounding noise
     assert np.abs(got - ref).max() <= 1e-5
     assert np.mean(np.abs(got - ref) <= 1e-12) > 0.99
+
+
+def test_cfg5_share_tta_predict_full_size():
+    """BASELINE.json configs[4] at one GPU's share of its 8-GPU batch: knn 5,
+    3 blocks, 32 768 poses x 3 TTA copies (flip + rotation) = 98 304 network
+    rows in batches of 32 768.  Size-independent checks, no oracle run:
+    (a) the device TTA path equals the inference.py pipeline fed from the host
+    (concatenate the copies, fixed-batch predict, data.undo, inference.py:70-111);
+    (b) a dataset holding every pose twice, predicted in batches twice as
+    large, gives each pose the same prediction as before -- in both halves
+    (batch-statistics BN and the undo / mean are invariant to duplication)."""
+    from lcn_amd.tta import augment_ops
+    N, bs = 32768, 32768
+    cfg = make_cfg(F=64, L=3, knn=5)
+    net = make_network(cfg, max_batch=2 * bs)
+    net.set_params(O.flatten(cfg, perturbed_params(cfg, seed=9)))
+    x, _ = _data(N, seed=12)
+    aug, undo, op_ord = augment_ops(flip=True, rotate=True)
+    net.dataset_upload(X_SLOT, x)
+    got = net.predict_dataset(X_SLOT, N, bs, augment=aug, undo=undo)
+    assert got.shape == (N, 51) and np.isfinite(got).all()
+    # (a) host-fed copies through the same network
+    cat = np.concatenate([x, O.flip_data(x), O.rotate_data(x)], axis=0)
+    preds, _ = _host_predict(net, cat, bs)
+    ref = O.undo(preds, op_ord, number_actions=2, translation=0.5)
+    assert np.abs(got - ref).max() <= 1e-5
+    assert np.mean(np.abs(got - ref) <= 1e-12) > 0.99
+    # (b) every pose twice, batches twice as large
+    net.dataset_upload(X_SLOT, np.concatenate([x, x], axis=0))
+    dup = net.predict_dataset(X_SLOT, 2 * N, 2 * bs, augment=aug, undo=undo)
+    np.testing.assert_array_equal(dup[:N], dup[N:])
+    assert np.abs(dup[:N] - got).max() <= 1e-5
+    net.close()

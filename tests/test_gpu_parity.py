@@ -364,3 +364,32 @@ def test_timers_cover_the_selected_kernel_classes_only():
     assert net.kernel_timing(native.K_GEMM_DW)[0] == 0
     assert loss1 == loss0
     net.close()
+
+
+def test_cfg4_full_batch_duplicated():
+    """BASELINE.json configs[3] whole on one GPU: exponential mask, F 256, 6
+    blocks, batch 131 072 as 65 536 poses taken twice.  Size-independent
+    property (no oracle run at this size): the outputs of both halves equal
+    those of the 65 536 batch, the loss and every gradient are unchanged
+    (BN-parameter gradients with the looser bar of the 8 192 -> 16 384 case)."""
+    cfg = make_cfg(F=256, L=6, knn=2, mask="exponential")
+    params = perturbed_params(cfg)
+    x, lab = synthetic_batch(65536, 2, seed=7)
+    net = make_network(cfg, max_batch=131072)
+    net.set_params(O.flatten(cfg, params))
+    out1 = net.forward(x)
+    l1, _ = net.train_step(x, lab, update=False, keep_grads=True)
+    g1 = net.get_grads()
+    x2, lab2 = np.concatenate([x, x]), np.concatenate([lab, lab])
+    out2 = net.forward(x2)
+    l2, _ = net.train_step(x2, lab2, update=False, keep_grads=True)
+    g2 = net.get_grads()
+    assert np.isfinite(out1).all() and np.isfinite(g1).all()
+    np.testing.assert_array_equal(out2[:65536], out2[65536:])
+    assert np.abs(out2[:65536] - out1).max() <= 1e-5
+    assert l2 == pytest.approx(l1, rel=1e-6)
+    for name, off, shape in net.param_layout():
+        n = int(np.prod(shape))
+        tol = 1e-3 if name.endswith(("_gamma", "_beta")) else 1e-4
+        assert rel_err(g2[off:off + n], g1[off:off + n]) < tol, name
+    net.close()
