@@ -28,9 +28,12 @@ __device__ __forceinline__ float leaky(float u, float alpha) { return fmaxf(u * 
 //   mode 0: (x, y)          mode 1: (x, y + x^2 / n_t)
 // fixed-order combines throughout (deterministic).  The finish kernels add
 // the kColSplit groups.
-__global__ __launch_bounds__(256) void colreduce_kernel(const float2* __restrict__ part,
-                                                        int n_tiles, int tile_rows, int B, int H,
-                                                        int mode, double2* __restrict__ out) {
+// publish = true: the sums are written through to memory (sc1 stores), for the
+// fused kernels below whose last workgroup reads every workgroup's sums
+template <bool kPublish>
+__device__ __forceinline__ void colreduce_body(const float2* __restrict__ part, int n_tiles,
+                                               int tile_rows, int B, int H, int mode,
+                                               double2* __restrict__ out) {
   __shared__ double2 red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + lane, p = blockIdx.y, P = gridDim.y;
@@ -49,9 +52,50 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const float2* __restrict
   }
   red[w][lane] = make_double2(a, b);
   __syncthreads();
-  if (w == 0 && col < H)
-    out[(size_t)p * H + col] = make_double2((red[0][lane].x + red[1][lane].x) + (red[2][lane].x + red[3][lane].x),
-                                            (red[0][lane].y + red[1][lane].y) + (red[2][lane].y + red[3][lane].y));
+  if (w == 0 && col < H) {
+    const double sx = (red[0][lane].x + red[1][lane].x) + (red[2][lane].x + red[3][lane].x);
+    const double sy = (red[0][lane].y + red[1][lane].y) + (red[2][lane].y + red[3][lane].y);
+    double2* o = out + (size_t)p * H + col;
+    if constexpr (kPublish) {
+      __hip_atomic_store(&o->x, sx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&o->y, sy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      *o = make_double2(sx, sy);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void colreduce_kernel(const float2* __restrict__ part,
+                                                        int n_tiles, int tile_rows, int B, int H,
+                                                        int mode, double2* __restrict__ out) {
+  colreduce_body<false>(part, n_tiles, tile_rows, B, H, mode, out);
+}
+
+// The column reduce and the BN finish in ONE launch: every workgroup publishes
+// its sums (write-through stores, drained by the storing wave) and draws a
+// ticket; the workgroup that draws the last one acquires (its CU's L1 is
+// invalidated, and it reads the sums with L1-bypassing loads) and runs the
+// finish that used to be a launch of its own.  One relaxed device-scope atomic
+// per workgroup, one acquire in the last workgroup only -- the form with a
+// device-scope fence in EVERY workgroup (release + acquire) measured ~9 us
+// slower per launch than the two kernels, because each release writes back an
+// XCD's L2, dirty from the GEMM before.  The last workgroup resets the ticket
+// for the next launch.  Returns true in the last workgroup (all its threads).
+__device__ __forceinline__ bool publish_and_draw(int* ticket, int total) {
+  __shared__ int is_last;
+  // only wave 0 stored; it drains its stores before its lane 0 draws
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = t == total - 1;
+    if (is_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  return is_last != 0;
 }
 
 void launch_colreduce(const float2* part, int n_tiles, int tile_rows, int B, int H, int mode,
@@ -63,14 +107,21 @@ void launch_colreduce(const float2* part, int n_tiles, int tile_rows, int B, int
 // Both finish kernels run as ONE workgroup of 1024 threads: first the
 // kColSplit tile groups of every column are added (fixed order) into LDS,
 // then one thread per channel adds its 17 joint columns and finishes.
-__device__ __forceinline__ void colsum_groups_lds(const double2* __restrict__ col, int H,
-                                                  double2* cs) {
+// kSameLaunch: the sums were published by other workgroups of this launch
+// (colreduce_body<true>): read them past the L1
+template <bool kSameLaunch = false>
+__device__ __forceinline__ void colsum_groups_lds(const double2* col, int H, double2* cs) {
   for (int c = threadIdx.x; c < H; c += blockDim.x) {
     double x = 0.0, y = 0.0;
     for (int p = 0; p < kColSplit; ++p) {
-      const double2 v = col[(size_t)p * H + c];
-      x += v.x;
-      y += v.y;
+      const double2* v = col + (size_t)p * H + c;
+      if constexpr (kSameLaunch) {
+        x += __hip_atomic_load(&v->x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        y += __hip_atomic_load(&v->y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        x += v->x;
+        y += v->y;
+      }
     }
     cs[c] = make_double2(x, y);
   }
@@ -114,16 +165,28 @@ struct ColSrc {
 // Forward BN finish per channel.  Phase 0: complete; 1: local channel sums ->
 // acc[2F] (and stop); 2: finish from the all-reduced acc.  zsum (when given)
 // receives the per-column sums of z (bias-gradient term of the backward).
-__global__ __launch_bounds__(1024) void bn_fwd_finalize_kernel(
-    ColSrc src, int H, int F, int phase, double rows,
-    const RowInfo* __restrict__ ri, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float eps, double* acc, BnStats st,
-    double* __restrict__ zsum, BnRider rider) {
-  extern __shared__ double2 cs[];  // [H]
+struct BnFwdArgs {
+  ColSrc src; int H, F, phase; double rows; const RowInfo* ri;
+  const float* gamma; const float* beta; float eps; double* acc; BnStats st; double* zsum;
+  BnRider rider;
+};
+template <bool kSameLaunch>
+__device__ __forceinline__ void bn_fwd_finish(const BnFwdArgs& a, double2* cs) {
+  const ColSrc src = a.src;
+  const int H = a.H, F = a.F, phase = a.phase;
+  const double rows = a.rows;
+  const RowInfo* ri = a.ri;
+  const float* gamma = a.gamma;
+  const float* beta = a.beta;
+  const float eps = a.eps;
+  double* acc = a.acc;
+  const BnStats st = a.st;
+  double* zsum = a.zsum;
+  const BnRider rider = a.rider;
   __shared__ double rows_sh;
   if (phase <= 1) {
     if (src.part) colsum_tiles_lds(src.part, src.n_tiles, src.tile_rows, src.B, H, 1, cs);
-    else colsum_groups_lds(src.col, H, cs);
+    else colsum_groups_lds<kSameLaunch>(src.col, H, cs);
   }
   const int J = H / F;
   double rows_global = rows;
@@ -176,13 +239,38 @@ __global__ __launch_bounds__(1024) void bn_fwd_finalize_kernel(
   }
 }
 
+__global__ __launch_bounds__(1024) void bn_fwd_finalize_kernel(BnFwdArgs a) {
+  extern __shared__ double2 cs[];  // [H]
+  bn_fwd_finish<false>(a, cs);
+}
+// colreduce (mode 1) + forward BN finish (phase 0 or 1) in one launch
+__global__ __launch_bounds__(256) void colreduce_bn_fwd_kernel(const float2* __restrict__ part,
+                                                               int n_tiles, int tile_rows, int B,
+                                                               double2* col, int* ticket,
+                                                               BnFwdArgs a) {
+  extern __shared__ double2 cs[];  // [H]
+  colreduce_body<true>(part, n_tiles, tile_rows, B, a.H, 1, col);
+  if (!publish_and_draw(ticket, gridDim.x * gridDim.y)) return;
+  bn_fwd_finish<true>(a, cs);
+}
+
 void launch_bn_fwd_finalize(const double2* col, const TilePartials& tp, int H, int F, int phase,
                             double rows, const RowInfo* ri, const float* gamma, const float* beta,
                             float eps, double* acc, BnStats st, double* zsum, const BnRider& rider,
                             hipStream_t s) {
   const ColSrc src{col, tp.part, tp.n_tiles, tp.tile_rows, tp.B};
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(1), dim3(1024), H * sizeof(double2), s, src, H,
-                     F, phase, rows, ri, gamma, beta, eps, acc, st, zsum, rider);
+  const BnFwdArgs a{src, H, F, phase, rows, ri, gamma, beta, eps, acc, st, zsum, rider};
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(1), dim3(1024), H * sizeof(double2), s, a);
+}
+
+void launch_colreduce_bn_fwd(const float2* part, int n_tiles, int tile_rows, int B, double2* col,
+                             int* ticket, int H, int F, int phase, double rows, const RowInfo* ri,
+                             const float* gamma, const float* beta, float eps, double* acc, BnStats st,
+                             double* zsum, const BnRider& rider, hipStream_t s) {
+  const ColSrc src{col, nullptr, 0, 0, 0};
+  const BnFwdArgs a{src, H, F, phase, rows, ri, gamma, beta, eps, acc, st, zsum, rider};
+  hipLaunchKernelGGL(colreduce_bn_fwd_kernel, dim3((H + 63) / 64, kColSplit), dim3(256),
+                     H * sizeof(double2), s, part, n_tiles, tile_rows, B, col, ticket, a);
 }
 
 // Backward BN finish per channel:  dz = c1*du + c2 + c3*z,
@@ -193,19 +281,34 @@ void launch_bn_fwd_finalize(const double2* col, const TilePartials& tp, int H, i
 // dgamma / dbeta / db are the LOCAL contributions (the raw-gradient vector is
 // all-reduced later); c123 uses the global sums.  bn = 0 (no BatchNorm):
 // dz = du and only db is written.  Phases as bn_fwd_finalize.
-__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
-    ColSrc src, int H, int F, int phase, int bn, double rows,
-    const RowInfo* __restrict__ ri, double b_local, const float* __restrict__ gamma,
-    const float* __restrict__ mean, const float* __restrict__ rstd, double* acc,
-    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ c123,
-    const double* __restrict__ zsum, float* __restrict__ db, BnRider rider) {
-  extern __shared__ double2 cs[];  // [H]
+struct BnBwdArgs {
+  ColSrc src; int H, F, phase, bn; double rows; const RowInfo* ri; double b_local;
+  const float* gamma; const float* mean; const float* rstd; double* acc;
+  float* dgamma; float* dbeta; float* c123; const double* zsum; float* db;
+  BnRider rider;
+};
+template <bool kSameLaunch>
+__device__ __forceinline__ void bn_bwd_finish(const BnBwdArgs& a, double2* cs) {
+  const ColSrc src = a.src;
+  const int H = a.H, F = a.F, phase = a.phase, bn = a.bn;
+  const double rows = a.rows, b_local = a.b_local;
+  const RowInfo* ri = a.ri;
+  const float* gamma = a.gamma;
+  const float* mean = a.mean;
+  const float* rstd = a.rstd;
+  double* acc = a.acc;
+  float* dgamma = a.dgamma;
+  float* dbeta = a.dbeta;
+  float* c123 = a.c123;
+  const double* zsum = a.zsum;
+  float* db = a.db;
+  const BnRider rider = a.rider;
   if (rider.kind == kRideLoss && threadIdx.x == 0) {
     if (phase == 1) acc[2 * F] = *rider.loss;
     else if (phase == 2) *rider.loss = acc[2 * F];
   }
   if (src.part) colsum_tiles_lds(src.part, src.n_tiles, src.tile_rows, src.B, H, 0, cs);
-  else colsum_groups_lds(src.col, H, cs);
+  else colsum_groups_lds<kSameLaunch>(src.col, H, cs);
   const int J = H / F;
   const double count = (ri ? ri->rows_global : rows) * (double)J;
   for (int ch = threadIdx.x; ch < F; ch += blockDim.x) {
@@ -241,15 +344,42 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
   }
 }
 
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(BnBwdArgs a) {
+  extern __shared__ double2 cs[];  // [H]
+  bn_bwd_finish<false>(a, cs);
+}
+// colreduce (mode 0) + backward BN finish (phase 0 or 1) in one launch
+__global__ __launch_bounds__(256) void colreduce_bn_bwd_kernel(const float2* __restrict__ part,
+                                                               int n_tiles, int tile_rows, int B,
+                                                               double2* col, int* ticket,
+                                                               BnBwdArgs a) {
+  extern __shared__ double2 cs[];  // [H]
+  colreduce_body<true>(part, n_tiles, tile_rows, B, a.H, 0, col);
+  if (!publish_and_draw(ticket, gridDim.x * gridDim.y)) return;
+  bn_bwd_finish<true>(a, cs);
+}
+
 void launch_bn_bwd_finalize(const double2* col, const TilePartials& tp, int H, int F, int phase,
                             int bn, double rows, const RowInfo* ri, double b_local,
                             const float* gamma, const float* mean, const float* rstd, double* acc,
                             float* dgamma, float* dbeta, float* c123, const double* zsum, float* db,
                             const BnRider& rider, hipStream_t s) {
   const ColSrc src{col, tp.part, tp.n_tiles, tp.tile_rows, tp.B};
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(1024), H * sizeof(double2), s, src, H,
-                     F, phase, bn, rows, ri, b_local, gamma, mean, rstd, acc, dgamma, dbeta, c123,
-                     zsum, db, rider);
+  const BnBwdArgs a{src, H, F, phase, bn, rows, ri, b_local, gamma, mean, rstd, acc, dgamma, dbeta,
+                    c123, zsum, db, rider};
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(1024), H * sizeof(double2), s, a);
+}
+
+void launch_colreduce_bn_bwd(const float2* part, int n_tiles, int tile_rows, int B, double2* col,
+                             int* ticket, int H, int F, int phase, int bn, double rows,
+                             const RowInfo* ri, double b_local, const float* gamma, const float* mean,
+                             const float* rstd, double* acc, float* dgamma, float* dbeta, float* c123,
+                             const double* zsum, float* db, const BnRider& rider, hipStream_t s) {
+  const ColSrc src{col, nullptr, 0, 0, 0};
+  const BnBwdArgs a{src, H, F, phase, bn, rows, ri, b_local, gamma, mean, rstd, acc, dgamma, dbeta,
+                    c123, zsum, db, rider};
+  hipLaunchKernelGGL(colreduce_bn_bwd_kernel, dim3((H + 63) / 64, kColSplit), dim3(256),
+                     H * sizeof(double2), s, part, n_tiles, tile_rows, B, col, ticket, a);
 }
 
 // h = [res +] leaky(scale*z + shift) over row-tiled [B][S*64] buffers; the

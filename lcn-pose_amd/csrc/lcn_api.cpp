@@ -117,6 +117,7 @@ struct Handle {
   int stat_rows = kGemmRows;      // rows per partial of the last GEMM: 128, or 32 (small-batch kernel)
   int small_rt = 0;               // launches of at most this many row tiles use the small-batch GEMM
   double2* colacc = nullptr;      // [kColSplit][H] float64 column sums
+  int* bn_ticket = nullptr;       // arrival counter of the fused colreduce + BN finish launches (0 between launches)
   float* dw_part = nullptr;
   size_t dw_cap = 0;              // floats in dw_part (sized for max_batch)
   double *loss_part = nullptr, *loss_sum = nullptr, *acc1 = nullptr, *acc2 = nullptr;
@@ -549,6 +550,7 @@ int build(Handle* h, const lcn_config* c) {
   CHECK(dalloc(h, &h->stat_part,
                (size_t)std::max<int64_t>(cdiv(B, kGemmRows), std::min<int64_t>(cdiv(B, kRT), h->small_rt)) * H));
   CHECK(dalloc(h, &h->colacc, (size_t)kColSplit * H));
+  CHECK(dalloc(h, &h->bn_ticket, 1));
   h->loss_grid = (int)std::min<int64_t>(2048, cdiv(B, 4));
   CHECK(dalloc(h, &h->loss_part, (size_t)h->loss_grid));
   CHECK(dalloc(h, &h->db_part, (size_t)h->loss_grid * 64));
@@ -696,10 +698,15 @@ int bn_stats(Handle* h, int k, int B) {
   const float* beta = h->theta + h->beta_off[k];
   const TilePartials tp = tile_partials(h, B);
   const BnRider none{};
-  if (!tp.part) launch_colreduce(h->stat_part, (int)cdiv(B, h->stat_rows), h->stat_rows, B, h->H, 1, h->colacc, s);
+  // many tiles: their column reduce and the finish (phase 0 / 1) are one launch
+  const int n_tiles = (int)cdiv(B, h->stat_rows);
   if (!h->phased && !multi(h)) {
-    launch_bn_fwd_finalize(h->colacc, tp, h->H, h->F, 0, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
-                           h->zsum[k], none, s);
+    if (!tp.part)
+      launch_colreduce_bn_fwd(h->stat_part, n_tiles, h->stat_rows, B, h->colacc, h->bn_ticket, h->H, h->F, 0,
+                              rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k], h->zsum[k], none, s);
+    else
+      launch_bn_fwd_finalize(h->colacc, tp, h->H, h->F, 0, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
+                             h->zsum[k], none, s);
     return LCN_OK;
   }
   // several ranks: BN layer 0's all-reduce also carries the ranks' batch rows
@@ -712,8 +719,12 @@ int bn_stats(Handle* h, int k, int B) {
     rider.b_local = rows;
     rider.ri_out = h->rowinfo;
   }
-  launch_bn_fwd_finalize(h->colacc, tp, h->H, h->F, 1, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
-                         h->zsum[k], rider, s);
+  if (!tp.part)
+    launch_colreduce_bn_fwd(h->stat_part, n_tiles, h->stat_rows, B, h->colacc, h->bn_ticket, h->H, h->F, 1,
+                            rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k], h->zsum[k], rider, s);
+  else
+    launch_bn_fwd_finalize(h->colacc, tp, h->H, h->F, 1, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
+                           h->zsum[k], rider, s);
   CHECK(allreduce(h, h->acc1, 2 * h->F + rider_slots(rider), ncclDouble));
   launch_bn_fwd_finalize(h->colacc, tp, h->H, h->F, 2, rows, ri, gamma, beta, h->eps, h->acc1, h->bn[k],
                          nullptr, rider, s);
@@ -926,10 +937,15 @@ int bn_back(Handle* h, int k, int B) {
   float* db = h->rg + h->b_off[k];
   const TilePartials tp = tile_partials(h, B);
   const BnRider none{};
-  if (!tp.part) launch_colreduce(h->stat_part, (int)cdiv(B, h->stat_rows), h->stat_rows, B, h->H, 0, h->colacc, s);
+  const int n_tiles = (int)cdiv(B, h->stat_rows);
   if ((!h->phased && !multi(h)) || !bn) {
-    launch_bn_bwd_finalize(h->colacc, tp, h->H, h->F, 0, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
-                           h->acc1, dgam, dbet, h->c123, h->zsum[k], db, none, s);
+    if (!tp.part)
+      launch_colreduce_bn_bwd(h->stat_part, n_tiles, h->stat_rows, B, h->colacc, h->bn_ticket, h->H, h->F, 0, bn,
+                              rows, ri, (double)B, gamma, st.mean, st.rstd, h->acc1, dgam, dbet, h->c123,
+                              h->zsum[k], db, none, s);
+    else
+      launch_bn_bwd_finalize(h->colacc, tp, h->H, h->F, 0, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
+                             h->acc1, dgam, dbet, h->c123, h->zsum[k], db, none, s);
     return LCN_OK;
   }
   // several ranks: the first BN backward of a step also carries the loss sum
@@ -939,8 +955,13 @@ int bn_back(Handle* h, int k, int B) {
     rider.loss = h->loss_sum;
     h->loss_pending = false;
   }
-  launch_bn_bwd_finalize(h->colacc, tp, h->H, h->F, 1, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
-                         h->acc1, dgam, dbet, h->c123, h->zsum[k], db, rider, s);
+  if (!tp.part)
+    launch_colreduce_bn_bwd(h->stat_part, n_tiles, h->stat_rows, B, h->colacc, h->bn_ticket, h->H, h->F, 1, bn,
+                            rows, ri, (double)B, gamma, st.mean, st.rstd, h->acc1, dgam, dbet, h->c123,
+                            h->zsum[k], db, rider, s);
+  else
+    launch_bn_bwd_finalize(h->colacc, tp, h->H, h->F, 1, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
+                           h->acc1, dgam, dbet, h->c123, h->zsum[k], db, rider, s);
   CHECK(allreduce(h, h->acc1, 2 * h->F + rider_slots(rider), ncclDouble));
   launch_bn_bwd_finalize(h->colacc, tp, h->H, h->F, 2, bn, rows, ri, (double)B, gamma, st.mean, st.rstd,
                          h->acc1, dgam, dbet, h->c123, h->zsum[k], db, rider, s);

@@ -370,6 +370,18 @@ void launch_bn_bwd_finalize(const double2* col, const TilePartials& tp, int H, i
                             const float* rstd, double* acc, float* dgamma, float* dbeta,
                             float* c123, const double* zsum, float* db, const BnRider& rider,
                             hipStream_t s);
+// colreduce and the finish (phase 0 or 1) in ONE launch: the workgroup that
+// finishes its column sums last runs the finish (kernels_elem.hip).  `ticket`:
+// a device int that is 0 before the launch (the kernel leaves it 0).
+void launch_colreduce_bn_fwd(const float2* part, int n_tiles, int tile_rows, int B, double2* col,
+                             int* ticket, int H, int F, int phase, double rows, const RowInfo* ri,
+                             const float* gamma, const float* beta, float eps, double* acc, BnStats st,
+                             double* zsum, const BnRider& rider, hipStream_t s);
+void launch_colreduce_bn_bwd(const float2* part, int n_tiles, int tile_rows, int B, double2* col,
+                             int* ticket, int H, int F, int phase, int bn, double rows,
+                             const RowInfo* ri, double b_local, const float* gamma, const float* mean,
+                             const float* rstd, double* acc, float* dgamma, float* dbeta, float* c123,
+                             const double* zsum, float* db, const BnRider& rider, hipStream_t s);
 // h = [res +] leaky(scale*z + shift), tiled [B][S*64] buffers
 void launch_bn_act(const float* z, const float* res, float* h, const float* scale,
                    const float* shift, int F, float alpha, int B, int S, const Dropout& drop,
