@@ -146,7 +146,7 @@ int main(int argc, char** argv) {
     a.alpha = 0.2f;
     a.Y = Y;
     a.S_out = J;
-    a.addsrc = fwd ? nullptr : Y;
+    a.addsrc = (fwd || std::getenv("LCN_DX_NORES")) ? nullptr : Y;
     a.epi_mode = kind >= 3 ? EPI_NONE : fwd ? EPI_BNFWD : EPI_BNBACK;
     a.stat = stat;
     a.epi_z = X2;

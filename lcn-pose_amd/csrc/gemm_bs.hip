@@ -24,8 +24,8 @@
 // coalesced 1 KB loads per input slab, prefetched one slab ahead in a second
 // register set); the weight block, shared by the 4 waves, goes into a double
 // LDS buffer by LDS-DMA, so there is one barrier per input slab.  The
-// accumulators start at bias + residual; the BN-backward epilogue's z is
-// loaded after the loop, ahead of the output stores (prefetching it at kernel
+// accumulators start at the bias; the residual and the BN-backward epilogue's z
+// are loaded after the loop, ahead of the output stores (prefetching it at kernel
 // start held 32 VGPRs through the loop and cost a wave per SIMD: 4 waves/SIMD
 // at <= 128 VGPRs is 3 % faster for the dX GEMM).  Measured
 // against a 128x64 LDS-staged tile with two barriers per slab: 124 vs 114
@@ -218,8 +218,12 @@ __global__ __launch_bounds__(64 * kGemmWaves) __attribute__((amdgpu_waves_per_eu
   int2 ia = kLift ? make_int2(0, so) : UIDX(beg), ib = ia;
   LOADW(ia.y, 0)
   LOADX(xa, ia.x)
-  // accumulators start at bias + residual (the MFMAs add onto them)
-  float4 bq[8], rq[8];
+  // accumulators start at the bias (the MFMAs add onto it); the residual is
+  // added after the loop, its loads in flight together with the epilogue's z
+  // (what the residual costs the dX GEMM is its 285 MB of traffic: 781 us with
+  // it, 757 us without; loading it ahead of the loop or after it measured the
+  // same, 784 vs 781 us)
+  float4 bq[8];
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
   if (a.bias) {
 #pragma unroll
@@ -227,13 +231,6 @@ __global__ __launch_bounds__(64 * kGemmWaves) __attribute__((amdgpu_waves_per_eu
   } else {
 #pragma unroll
     for (int q = 0; q < 8; ++q) bq[q] = zero4;
-  }
-  if (a.addsrc) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) rq[q] = BUFLD(OUT_RES(a.addsrc), xlo + (q & 3) * 1024, so * 8192 + (q >> 2) * 4096);
-  } else {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) rq[q] = zero4;
   }
   if constexpr (PRO == PRO_BNACT) {  // BN scale / shift of the operand's layer -> LDS
     float* tb = (float*)(Wl + kTabOff);
@@ -256,11 +253,9 @@ __global__ __launch_bounds__(64 * kGemmWaves) __attribute__((amdgpu_waves_per_eu
   f32x16 acc0, acc1;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const float4 b0 = bq[q], b1 = bq[4 + q], r0 = rq[q], r1 = rq[4 + q];
-    acc0[4 * q + 0] = b0.x + r0.x; acc0[4 * q + 1] = b0.y + r0.y;
-    acc0[4 * q + 2] = b0.z + r0.z; acc0[4 * q + 3] = b0.w + r0.w;
-    acc1[4 * q + 0] = b1.x + r1.x; acc1[4 * q + 1] = b1.y + r1.y;
-    acc1[4 * q + 2] = b1.z + r1.z; acc1[4 * q + 3] = b1.w + r1.w;
+    const float4 b0 = bq[q], b1 = bq[4 + q];
+    acc0[4 * q + 0] = b0.x; acc0[4 * q + 1] = b0.y; acc0[4 * q + 2] = b0.z; acc0[4 * q + 3] = b0.w;
+    acc1[4 * q + 0] = b1.x; acc1[4 * q + 1] = b1.y; acc1[4 * q + 2] = b1.z; acc1[4 * q + 3] = b1.w;
   }
   __syncthreads();
   // every output slab has >= 1 input block (checked in lcn_create)
@@ -290,8 +285,13 @@ __global__ __launch_bounds__(64 * kGemmWaves) __attribute__((amdgpu_waves_per_eu
     // z of the layer below, issued before the output stores so its latency
     // overlaps them (keeping it live through the loop would cost 32 VGPRs,
     // i.e. a wave per SIMD of occupancy)
+#ifdef EXP_DX_NOZ  // diagnostic: the epilogue's z tile comes from one hot tile (no HBM traffic, no miss latency)
+    const __amdgpu_buffer_rsrc_t zres = __builtin_amdgcn_make_buffer_rsrc((void*)a.epi_z, 0, S_out * 8192, 0x00020000);
+    const int zo = 0;
+#else
     const __amdgpu_buffer_rsrc_t zres = OUT_RES(a.epi_z);
     const int zo = so * 8192;
+#endif
     zp0 = BUFLD(zres, xlo, zo);        zp1 = BUFLD(zres, xlo + 1024, zo);
     zp2 = BUFLD(zres, xlo + 2048, zo); zp3 = BUFLD(zres, xlo + 3072, zo);
     zp4 = BUFLD(zres, xlo, zo + 4096);        zp5 = BUFLD(zres, xlo + 1024, zo + 4096);
@@ -300,6 +300,16 @@ __global__ __launch_bounds__(64 * kGemmWaves) __attribute__((amdgpu_waves_per_eu
   float v[32];
 #pragma unroll
   for (int k = 0; k < 16; ++k) { v[k] = acc0[k]; v[16 + k] = acc1[k]; }
+  if (a.addsrc) {  // residual: Y = acc + addsrc (addsrc may be Y itself: each lane reads what it then writes)
+    const __amdgpu_buffer_rsrc_t rres = OUT_RES(a.addsrc);
+    float4 rq[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) rq[q] = BUFLD(rres, xlo + (q & 3) * 1024, so * 8192 + (q >> 2) * 4096);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      v[4 * q + 0] += rq[q].x; v[4 * q + 1] += rq[q].y; v[4 * q + 2] += rq[q].z; v[4 * q + 3] += rq[q].w;
+    }
+  }
   if (live) {
     const __amdgpu_buffer_rsrc_t yres = OUT_RES(a.Y);
 #pragma unroll
@@ -460,7 +470,11 @@ __global__ __launch_bounds__(64 * kGemmWaves) __attribute__((amdgpu_waves_per_eu
     return acc;
   };
   float P_ = 0.f, Q_ = 0.f;
+#ifdef EXP_DX_NOSUM  // diagnostic: no column-sum passes (the z tile is still loaded and consumed)
+  P_ = zp0.x + zp1.x + zp2.x + zp3.x + zp4.x + zp5.x + zp6.x + zp7.x + v[lane & 31];
+#else
   BNBACK_EPI(zp)
+#endif
 #undef BNBACK_EPI
   comb[(w * 64 + c) * 3 + 0] = P_;
   comb[(w * 64 + c) * 3 + 1] = Q_;

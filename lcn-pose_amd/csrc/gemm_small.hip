@@ -159,8 +159,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bs_small_kernel(GemmArgs a) {
       const float4 r = ((const float4*)a.addsrc)[tbase + q * 64];
       add.x += r.x; add.y += r.y; add.z += r.z; add.w += r.w;
     }
-    // gemm_bs_kernel seeds the accumulators with bias + residual; adding them
-    // last instead differs in rounding only
+    // gemm_bs_kernel seeds the accumulators with the bias and adds the residual
+    // last; adding both last differs in rounding only
     v[4 * q] += add.x; v[4 * q + 1] += add.y; v[4 * q + 2] += add.z; v[4 * q + 3] += add.w;
   }
   {

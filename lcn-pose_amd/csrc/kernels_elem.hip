@@ -74,8 +74,9 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const float2* __restrict
 // The column reduce and the BN finish in ONE launch: every workgroup publishes
 // its sums (write-through stores, drained by the storing wave) and draws a
 // ticket; the workgroup that draws the last one acquires (its CU's L1 is
-// invalidated, and it reads the sums with L1-bypassing loads) and runs the
-// finish that used to be a launch of its own.  One relaxed device-scope atomic
+// invalidated) and runs the
+// finish that used to be a launch of its own (plain loads after the acquire and
+// a workgroup barrier).  One relaxed device-scope atomic
 // per workgroup, one acquire in the last workgroup only -- the form with a
 // device-scope fence in EVERY workgroup (release + acquire) measured ~9 us
 // slower per launch than the two kernels, because each release writes back an
@@ -108,20 +109,20 @@ void launch_colreduce(const float2* part, int n_tiles, int tile_rows, int B, int
 // kColSplit tile groups of every column are added (fixed order) into LDS,
 // then one thread per channel adds its 17 joint columns and finishes.
 // kSameLaunch: the sums were published by other workgroups of this launch
-// (colreduce_body<true>): read them past the L1
+// (colreduce_body<true>) and this workgroup has acquired (publish_and_draw): its
+// plain loads miss the invalidated L1 and find the written-through sums.  One
+// thread per column, the kColSplit loads of a column in flight together.
 template <bool kSameLaunch = false>
 __device__ __forceinline__ void colsum_groups_lds(const double2* col, int H, double2* cs) {
   for (int c = threadIdx.x; c < H; c += blockDim.x) {
+    double2 v[kColSplit];
+#pragma unroll
+    for (int p = 0; p < kColSplit; ++p) v[p] = col[(size_t)p * H + c];
     double x = 0.0, y = 0.0;
+#pragma unroll
     for (int p = 0; p < kColSplit; ++p) {
-      const double2* v = col + (size_t)p * H + c;
-      if constexpr (kSameLaunch) {
-        x += __hip_atomic_load(&v->x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        y += __hip_atomic_load(&v->y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        x += v->x;
-        y += v->y;
-      }
+      x += v[p].x;
+      y += v[p].y;
     }
     cs[c] = make_double2(x, y);
   }
