@@ -168,7 +168,7 @@ constexpr int kDwRounds = 4;
 inline DwPlan make_dw_plan(int64_t B, int groups, int slots, int chunks, int max_slots) {
   DwPlan p{};
   const int64_t n64 = (B + 63) / 64;
-  if (groups * 8 <= slots && 8 * kDwRounds <= max_slots) {
+  if (groups * 8 <= slots && 8 * kDwRounds <= max_slots && n64 >= 16) {  // (a tiny batch: plain chunks)
     // >= 64 items per XCD where the batch allows (16 for the shortest round), at most 256 rows an item
     const int64_t r = B / (8 * 64);
     p.item_rows = (int)std::min<int64_t>(256, std::max<int64_t>(64, r / 64 * 64));
