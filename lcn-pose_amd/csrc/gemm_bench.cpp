@@ -108,6 +108,12 @@ int main(int argc, char** argv) {
   int* dfo = dev(by_length(fptr));
   int* dbo = dev(by_length(bptr));
   const int tail = std::getenv("LCN_GEMM_TAIL") ? std::atoi(std::getenv("LCN_GEMM_TAIL")) : 16;
+  // variant 1: two output slabs per workgroup (gemm_pair.hip)
+  const PairPlan fpp = make_pair_plan(fptr, fidx, J), bpp = make_pair_plan(bptr, bidx, J);
+  int4 *dfpp = dev(fpp.pairs), *dbpp = dev(bpp.pairs), *dfpm = dev(fpp.ment), *dbpm = dev(bpp.ment);
+  int *dfpo = dev(fpp.order), *dbpo = dev(bpp.order);
+  std::printf("pairs: %zu forward (%d of %d activation loads saved), %zu backward (%d saved)\n", fpp.pairs.size(), fpp.saved,
+              nblk, bpp.pairs.size(), bpp.saved);
   float* Y;
   CK(hipMalloc(&Y, (size_t)B * H * 4));
   float2* stat;
@@ -158,7 +164,12 @@ int main(int argc, char** argv) {
     a.B = B;
     a.n_out_slabs = J;
     a.n_rt = (B + kRT - 1) / kRT;
-    (void)variant;
+    if (variant == 1) {
+      a.pairs = fwd ? dfpp : dbpp;
+      a.ment = fwd ? dfpm : dbpm;
+      a.pair_order = tail > 0 ? (fwd ? dfpo : dbpo) : nullptr;
+      a.n_pairs = (int)(fwd ? fpp : bpp).pairs.size();
+    }
     a.n_blocks = nblk;
     return a;
   };
@@ -236,7 +247,9 @@ int main(int argc, char** argv) {
           launch_gemm_dw(d, s);
           launch_dw_reduce(part, dw_plan_slots(d.plan), nblk, dblk, dW, H, H, H, s);
         } else {
-          launch_gemm_bs(mk(c.kind, c.pro, c.variant), s);
+          const GemmArgs ga = mk(c.kind, c.pro, c.variant);
+          if (ga.pairs) launch_gemm_bs_pair(ga, s);
+          else launch_gemm_bs(ga, s);
         }
       };
       run();

@@ -71,6 +71,9 @@ struct Handle {
   int nblk = 0;
   int *fwd_ptr = nullptr, *bwd_ptr = nullptr;
   int *fwd_order = nullptr, *bwd_order = nullptr;   // output slabs by falling list length
+  // pairs of output slabs of the hidden layers' forward / backward-data GEMMs (PairPlan)
+  struct PairDev { int4* pairs = nullptr; int4* ment = nullptr; int* order = nullptr; int n = 0; };
+  PairDev fwd_pair, bwd_pair;
   int2 *fwd_idx = nullptr, *bwd_idx = nullptr, *blk = nullptr;
   int *thin_ptr = nullptr, *out_ptr = nullptr;                  // thin layers (padded slab)
   int2 *thin_idx = nullptr, *out_idx = nullptr, *lift_blk = nullptr, *out_blk = nullptr;
@@ -233,6 +236,8 @@ int upload(Handle* h, T** p, const std::vector<T>& src) {
 }
 
 int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+int gemm_pair_mode();
 
 // Pair the blocks of each output slab into weight-gradient work groups
 // (so, block0, block1 | -1, rank | count << 8): the group's rank among the
@@ -400,6 +405,23 @@ int build(Handle* h, const lcn_config* c) {
   };
   CHECK(upload(h, &h->fwd_order, by_length(fptr)));
   CHECK(upload(h, &h->bwd_order, by_length(bptr)));
+  // Two output slabs per workgroup pay where a joint has several slabs (their
+  // lists are identical: half the activation loads; the cfg4 shape's forward
+  // GEMM 4.57 -> 4.43 ms).  With one slab per joint (41 % of the loads saved at
+  // knn 3) the shorter loop is offset by two epilogues in a row at three
+  // workgroups per CU: forward +-0, backward-data +2.5 % in the cfg3 step.
+  if (const int pm = gemm_pair_mode(); pm == 1 || (pm < 0 && h->spj > 1)) {
+    auto up = [&](const std::vector<int>& ptr, const std::vector<int2>& idx, Handle::PairDev* d) {
+      const PairPlan pp = make_pair_plan(ptr, idx, h->nslab);
+      CHECK(upload(h, &d->pairs, pp.pairs));
+      CHECK(upload(h, &d->ment, pp.ment));
+      CHECK(upload(h, &d->order, pp.order));
+      d->n = (int)pp.pairs.size();
+      return (int)LCN_OK;
+    };
+    CHECK(up(fptr, fidx, &h->fwd_pair));
+    CHECK(up(bptr, bidx, &h->bwd_pair));
+  }
   for (int so = 0; so < h->nslab; ++so)
     if (fptr[so + 1] == fptr[so]) {
       h->err = "output joint " + std::to_string(so / h->spj) + " has no input joint in the mask";
@@ -753,6 +775,7 @@ struct GemmCall {
   int timer; double flops_per_row;
   const int* order = nullptr;   // tail schedule (hidden layers); null: natural order
   int k_groups = 0;             // non-zero 8-feature groups of the input slab (the lift), 0 = all
+  const Handle::PairDev* pair = nullptr;  // hidden layers: pairs of output slabs, or null
 };
 
 // row-tile groups per XCD issued longest-list-first at the end of a launch
@@ -760,6 +783,14 @@ struct GemmCall {
 int tail_groups() {
   static const int t = std::getenv("LCN_GEMM_TAIL") ? std::atoi(std::getenv("LCN_GEMM_TAIL")) : 16;
   return t;
+}
+
+// two output slabs per workgroup for the hidden layers' large launches
+// (gemm_pair.hip): LCN_GEMM_PAIR=1 always, 0 never, unset: where a joint has
+// several slabs.  Read at handle creation.
+int gemm_pair_mode() {
+  const char* e = std::getenv("LCN_GEMM_PAIR");
+  return e ? (std::atoi(e) != 0) : -1;
 }
 
 int gemm(Handle* h, const GemmCall& c, int B) {
@@ -810,7 +841,14 @@ int gemm(Handle* h, const GemmCall& c, int B) {
   h->stat_rows = small ? kRT : kGemmRows;
   hipEvent_t ev[2];
   if (c.timer >= 0) tstart(h, c.timer, ev);
+  if (!small && c.pair && c.pair->n > 0) {
+    a.pairs = c.pair->pairs;
+    a.ment = c.pair->ment;
+    a.pair_order = c.pair->order;
+    a.n_pairs = c.pair->n;
+  }
   if (small) launch_gemm_bs_small(a, h->stream);
+  else if (a.pairs) launch_gemm_bs_pair(a, h->stream);
   else launch_gemm_bs(a, h->stream);
   if (c.timer >= 0) tstop(h, c.timer, ev, c.flops_per_row * B);
   return LCN_OK;
@@ -826,6 +864,7 @@ int gemm_hidden(Handle* h, int k, int kindt, const Operand& X, float* Y, const f
              Y, h->nslab, addsrc, epi_mode, epi_layer,
              kindt, 2.0 * 4096.0 * h->nblk,   // 2*64*64 FLOP per block per row
              fwd ? h->fwd_order : h->bwd_order};
+  c.pair = fwd ? &h->fwd_pair : &h->bwd_pair;
   return gemm(h, c, B);
 }
 

@@ -134,12 +134,121 @@ struct GemmArgs {
   int epi_F;                         // channels of the epi_* vectors (spj of Y = epi_F/64)
   Dropout epi_drop;                  // EPI_BNBACK: dropout of the layer below (rate 0 = off)
   int B; int n_out_slabs; int n_rt;  // n_rt = ceil(B / 32)
+  // two output slabs per workgroup (gemm_pair.hip; PairPlan below), or null
+  const int4* pairs;                 // [n_pairs]: (slab A, slab B or -1, first merged entry, end)
+  const int4* ment;                  // merged entries: (input slab, block of A or -1, block of B or -1, 0)
+  const int* pair_order;             // pairs by falling step count (tail schedule), or null
+  int n_pairs;
 };
 void launch_gemm_bs(const GemmArgs& a, hipStream_t s);
+// the hidden layers with a.pairs set: one workgroup per (row-tile group, pair of output slabs)
+void launch_gemm_bs_pair(const GemmArgs& a, hipStream_t s);
 // the same for launches of few row tiles (gemm_small.hip): one row tile per
 // workgroup, the slab list split over its waves; stat gets one partial per
 // 32-row tile (not per 128-row group); no dropout epilogue
 void launch_gemm_bs_small(const GemmArgs& a, hipStream_t s);
+
+// Pairs of output slabs for gemm_bs_pair_kernel.  A workgroup walks the union
+// of its two slabs' input lists and loads an input slab both lists hold once,
+// so the slabs are paired for the largest total overlap: slabs with identical
+// lists first (the slabs of one joint when a joint has several), then an exact
+// maximum-weight matching of the rest (bitmask DP, up to 20 slabs; greedy
+// beyond), a slab that finds no partner runs alone (slab B = -1).
+//   ptr / idx: the CSR lists of launch_gemm_bs (output slab -> (input slab, block)),
+//   input slabs ascending within a list.
+struct PairPlan {
+  std::vector<int4> pairs;   // (slab A, slab B or -1, first merged entry, end)
+  std::vector<int4> ment;    // (input slab, block of A or -1, block of B or -1, 0), input slabs ascending
+  std::vector<int> order;    // pair indices by falling number of block steps
+  int saved = 0;             // activation loads saved per row tile (sum of the pairs' overlaps)
+};
+inline PairPlan make_pair_plan(const std::vector<int>& ptr, const std::vector<int2>& idx, int nslab) {
+  auto list_of = [&](int so) {
+    std::vector<int> l;
+    for (int e = ptr[so]; e < ptr[so + 1]; ++e) l.push_back(idx[e].x);
+    return l;
+  };
+  std::vector<std::vector<int>> L(nslab);
+  for (int s = 0; s < nslab; ++s) L[s] = list_of(s);
+  auto overlap = [&](int x, int y) {
+    int n = 0;
+    size_t i = 0, j = 0;
+    while (i < L[x].size() && j < L[y].size()) {
+      if (L[x][i] == L[y][j]) { ++n; ++i; ++j; }
+      else if (L[x][i] < L[y][j]) ++i;
+      else ++j;
+    }
+    return n;
+  };
+  std::vector<std::pair<int, int>> pr;
+  std::vector<int> rest;
+  std::vector<char> used(nslab, 0);
+  for (int s = 0; s < nslab; ++s) {  // identical lists pair up
+    if (used[s]) continue;
+    int mate = -1;
+    for (int u = s + 1; u < nslab && mate < 0; ++u)
+      if (!used[u] && L[u] == L[s]) mate = u;
+    if (mate >= 0) { used[s] = used[mate] = 1; pr.push_back({s, mate}); }
+  }
+  for (int s = 0; s < nslab; ++s) if (!used[s]) rest.push_back(s);
+  const int n = (int)rest.size();
+  if (n <= 20) {  // exact: best[mask] = largest total overlap of the slabs in mask
+    std::vector<int> best((size_t)1 << n, 0), choice((size_t)1 << n, -1);
+    for (unsigned mask = 1; mask < (1u << n); ++mask) {
+      const int i = __builtin_ctz(mask);
+      const unsigned r = mask & ~(1u << i);
+      best[mask] = best[r];  // slab i alone
+      choice[mask] = -1;
+      for (unsigned m = r; m; m &= m - 1) {
+        const int j = __builtin_ctz(m);
+        const int v = best[r & ~(1u << j)] + overlap(rest[i], rest[j]);
+        if (v > best[mask]) { best[mask] = v; choice[mask] = j; }
+      }
+    }
+    for (unsigned mask = n ? (1u << n) - 1 : 0; mask;) {
+      const int i = __builtin_ctz(mask), j = choice[mask];
+      pr.push_back({rest[i], j >= 0 ? rest[j] : -1});
+      mask &= ~(1u << i);
+      if (j >= 0) mask &= ~(1u << j);
+    }
+  } else {
+    std::vector<char> done(n, 0);
+    for (;;) {
+      int bi = -1, bj = -1, bv = 0;
+      for (int i = 0; i < n; ++i)
+        for (int j = i + 1; j < n; ++j)
+          if (!done[i] && !done[j] && overlap(rest[i], rest[j]) > bv) { bv = overlap(rest[i], rest[j]); bi = i; bj = j; }
+      if (bi < 0) break;
+      done[bi] = done[bj] = 1;
+      pr.push_back({rest[bi], rest[bj]});
+    }
+    for (int i = 0; i < n; ++i) if (!done[i]) pr.push_back({rest[i], -1});
+  }
+  std::sort(pr.begin(), pr.end());
+  PairPlan p;
+  std::vector<int> steps;
+  for (const auto& q : pr) {
+    const int A = q.first, B = q.second;
+    const int beg = (int)p.ment.size();
+    int ea = ptr[A], eb = B >= 0 ? ptr[B] : 0;
+    const int enda = ptr[A + 1], endb = B >= 0 ? ptr[B + 1] : 0;
+    while (ea < enda || eb < endb) {
+      const int sa = ea < enda ? idx[ea].x : INT32_MAX, sb = eb < endb ? idx[eb].x : INT32_MAX;
+      const int si = sa < sb ? sa : sb;
+      int4 m = make_int4(si, -1, -1, 0);
+      if (sa == si) m.y = idx[ea++].y;
+      if (sb == si) m.z = idx[eb++].y;
+      if (m.y >= 0 && m.z >= 0) ++p.saved;
+      p.ment.push_back(m);
+    }
+    p.pairs.push_back(make_int4(A, B, beg, (int)p.ment.size()));
+    steps.push_back((enda - ptr[A]) + (endb - (B >= 0 ? ptr[B] : 0)));
+  }
+  p.order.resize(p.pairs.size());
+  for (size_t i = 0; i < p.order.size(); ++i) p.order[i] = (int)i;
+  std::stable_sort(p.order.begin(), p.order.end(), [&](int x, int y) { return steps[x] > steps[y]; });
+  return p;
+}
 
 // How a weight-gradient launch splits the batch (kernels_gemm.hip).  The batch
 // is cut into items of item_rows rows (a multiple of 32).  A workgroup is

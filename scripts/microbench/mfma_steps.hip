@@ -15,6 +15,11 @@
 //           register per lane instead of a 64-bit address pair), activations
 //           and LDS-DMA alike
 //   mode 8  mode 7 with the loads spread between the MFMAs as in mode 6
+//   mode 9  mode 7 with two accumulator pairs (two output slabs per wave): the
+//           activation fragments are loaded on every other iteration only (both
+//           output slabs multiply the same input slab), the weight DMA on every one
+//   mode 10 mode 9's register shape (two accumulator pairs, alternating) with
+//           the activation loads on every iteration: the control for mode 9
 // 4 workgroups of 4 waves per CU as in the GEMM.  Results are meaningless; only
 // the rate matters.
 //   hipcc --offload-arch=gfx950 -O3 -o mfma_steps mfma_steps.hip && ./mfma_steps
@@ -45,8 +50,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   __shared__ __attribute__((aligned(16))) float4 Wa[(MODE == 5 || MODE == 6) ? 1024 : 1];
   __shared__ __attribute__((aligned(16))) float4 Wb[(MODE == 5 || MODE == 6) ? 1024 : 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  f32x16 acc0, acc1;
-  for (int k = 0; k < 16; ++k) { acc0[k] = 0.f; acc1[k] = 0.f; }
+  f32x16 acc0, acc1, acc2, acc3;
+  for (int k = 0; k < 16; ++k) { acc0[k] = 0.f; acc1[k] = 0.f; acc2[k] = 0.f; acc3[k] = 0.f; }
   float4 xa[8], xb[8];
   for (int g = 0; g < 8; ++g) {
     xa[g] = make_float4(1e-3f * lane, 1e-3f * g, 1.f, 2.f);
@@ -70,7 +75,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)X, 0, n_tiles * 8192, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, 175 * 16384, 0x00020000);
 #define LOADXM(P, IT)                                                     \
-  if ((MODE == 7 || MODE == 8)) {                                                        \
+  if ((MODE >= 7)) {                                                        \
     const int u_ = (int)(utile(IT) * 16u);                                \
     _Pragma("unroll") for (int g = 0; g < 8; ++g) {                       \
       const v4f v_ = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(xr, u_, g * 1024, 0)); \
@@ -96,9 +101,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
       STEP(w0, w1, x[g])
     }
+    if (MODE == 9 || MODE == 10) {
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+      }
+    }
   };
   auto loadw = [&](int it, int buf) {
-    if ((MODE == 7 || MODE == 8)) {
+    if ((MODE >= 7)) {
       const int off = (int)(((unsigned)((blockIdx.x + 7 * it) % 175) * 1024u + threadIdx.x) * 16u);
       float4* d = Wl + buf * 1024 + (threadIdx.x & ~63);
 #pragma unroll
@@ -121,6 +133,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     SGB(0x020, 1) SGB(0x008, 5) SGB(0x020, 1) SGB(0x008, 5) SGB(0x020, 1) SGB(0x008, 5)  \
     SGB(0x008, 4)                                                                        \
   }
+#define STEP2(W0, W1, XV)                \
+  acc2 = MFMA32((W0).x, (XV).x, acc2);   \
+  acc3 = MFMA32((W1).x, (XV).x, acc3);   \
+  acc2 = MFMA32((W0).y, (XV).y, acc2);   \
+  acc3 = MFMA32((W1).y, (XV).y, acc3);   \
+  acc2 = MFMA32((W0).z, (XV).z, acc2);   \
+  acc3 = MFMA32((W1).z, (XV).z, acc3);   \
+  acc2 = MFMA32((W0).w, (XV).w, acc2);   \
+  acc3 = MFMA32((W1).w, (XV).w, acc3);
+  auto compute2 = [&](int buf, float4 (&x)[8]) {
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const float4 w0 = Wl[buf * 1024 + (2 * g) * 64 + lane];
+      const float4 w1 = Wl[buf * 1024 + (2 * g + 1) * 64 + lane];
+      STEP2(w0, w1, x[g])
+    }
+    // two fragment reads ahead of each group of eight MFMAs (keeps the reads from
+    // being hoisted into one block of 64 registers)
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    }
+  };
+  if (MODE == 9 || MODE == 10) {
+    // iterations come in fours: (xa, slab 0) (xa, slab 1) (xb, slab 0) (xb, slab 1)
+    for (int it = 0; it < iters; it += 4) {
+      loadw(it + 1, 1);
+      LOADXM(xb, it + 2)
+      compute(0, xa);
+      __syncthreads();
+      loadw(it + 2, 0);
+      if (MODE == 10) { LOADXM(xa, it + 3) }
+      compute2(1, MODE == 10 ? xb : xa);
+      __syncthreads();
+      loadw(it + 3, 1);
+      LOADXM(xa, it + 4)
+      compute(0, MODE == 10 ? xa : xb);
+      __syncthreads();
+      loadw(it + 4, 0);
+      if (MODE == 10) { LOADXM(xb, it + 5) }
+      compute2(1, xb);
+      __syncthreads();
+    }
+  } else
   for (int it = 0; it < iters; it += 2) {
     if (MODE >= 4) loadw(it + 1, 1);
     LOADXM(xb, it + 1)
@@ -136,7 +193,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (MODE >= 1) __syncthreads();
   }
   float s = 0.f;
-  for (int k = 0; k < 16; ++k) s += acc0[k] + acc1[k];
+  for (int k = 0; k < 16; ++k) s += acc0[k] + acc1[k] + acc2[k] + acc3[k];
   out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
@@ -185,6 +242,10 @@ int main(int argc, char** argv) {
   run<8>(iters, X, W, n_tiles, out, grid);
   run<7, 3>(iters, X, W, n_tiles, out, grid);
   run<8, 3>(iters, X, W, n_tiles, out, grid);
+  run<9, 3>(iters, X, W, n_tiles, out, grid);
+  run<10, 3>(iters, X, W, n_tiles, out, grid);
+  run<9, 2>(iters, X, W, n_tiles, out, grid);
+  run<10, 2>(iters, X, W, n_tiles, out, grid);
   run<7, 2>(iters, X, W, n_tiles, out, grid);
   run<8, 2>(iters, X, W, n_tiles, out, grid);
   return 0;

@@ -35,11 +35,14 @@ CASES = [
 
 # Batches of up to 2560 rows run the small-batch GEMM kernel (gemm_small.hip);
 # LCN_SMALL_RT=0 at handle creation keeps such a batch on the large-batch
-# kernel (gemm_bs.hip), so both are held to the oracle on the same cases.
-@pytest.fixture(params=["small_batch_gemm", "large_batch_gemm"])
+# kernels: one output slab per workgroup (gemm_bs.hip, LCN_GEMM_PAIR=0) or two
+# (gemm_pair.hip, LCN_GEMM_PAIR=1), so all three are held to the oracle on the
+# same cases.
+@pytest.fixture(params=["small_batch_gemm", "large_batch_gemm", "paired_slab_gemm"])
 def gemm_path(request, monkeypatch):
-    if request.param == "large_batch_gemm":
+    if request.param != "small_batch_gemm":
         monkeypatch.setenv("LCN_SMALL_RT", "0")
+        monkeypatch.setenv("LCN_GEMM_PAIR", "1" if request.param == "paired_slab_gemm" else "0")
     return request.param
 
 
@@ -279,12 +282,15 @@ def test_cfg4_shape_matches_oracle():
     assert not bad, bad
 
 
-@pytest.mark.parametrize("L,B,rate", [(3, 256, 0.3), (1, 200, 0.25)])
-def test_dropout_training_step_matches_oracle(L, B, rate):
+@pytest.mark.parametrize("L,B,rate,pair", [(3, 256, 0.3, "0"), (1, 200, 0.25, "0"), (2, 256, 0.3, "1")])
+def test_dropout_training_step_matches_oracle(L, B, rate, pair, monkeypatch):
     """tf.nn.dropout after every BN + LeakyReLU (models_att.py:673, 700, 742)
     with the counter-based masks (oracle.dropout_mask): loss and every
     gradient of two consecutive training steps (mask step 0, then 1) against
-    the float64 oracle; predict is unaffected by the dropout setting."""
+    the float64 oracle; predict is unaffected by the dropout setting.  A step
+    with dropout always takes a large-batch GEMM kernel: one output slab per
+    workgroup, or two (pair)."""
+    monkeypatch.setenv("LCN_GEMM_PAIR", pair)
     cfg, params, x, lab, net = _setup(dict(F=64, L=L, knn=3), B)
     seed = 0x1234_5678_9ABC
     net.set_dropout(rate, seed)
