@@ -24,6 +24,16 @@ __device__ __forceinline__ float4 bnact4(float4 v, float4 sc, float4 sh, float a
   return v;
 }
 
+// The same with the tables pre-scaled by a = (1 + alpha) / 2 and ba = (1 - alpha) / (1 + alpha):
+// leaky(u) = a u + ((1 - alpha) / 2) |u| = u' + ba |u'| for u' = a u -- two operations an element
+__device__ __forceinline__ float4 bnact4_scaled(float4 v, float4 sc, float4 sh, float ba) {
+  v.x = fmaf(v.x, sc.x, sh.x); v.x = fmaf(fabsf(v.x), ba, v.x);
+  v.y = fmaf(v.y, sc.y, sh.y); v.y = fmaf(fabsf(v.y), ba, v.y);
+  v.z = fmaf(v.z, sc.z, sh.z); v.z = fmaf(fabsf(v.z), ba, v.z);
+  v.w = fmaf(v.w, sc.w, sh.w); v.w = fmaf(fabsf(v.w), ba, v.w);
+  return v;
+}
+
 // BN + LeakyReLU backward:
 //   u = scale*z + shift,  du = u > 0 ? dh : alpha*dh,  dz = c1*du + c2 + c3*z
 struct BnBackCoef { float4 sc, sh, c1, c2, c3; };
@@ -52,6 +62,21 @@ __device__ __forceinline__ float4 bnback4(float4 dh, float4 z, const BnBackCoef&
   r.y = bnback1(dh.y, z.y, c.sc.y, c.sh.y, c.c1.y, c.c2.y, c.c3.y, alpha);
   r.z = bnback1(dh.z, z.z, c.sc.z, c.sh.z, c.c1.z, c.c2.z, c.c3.z, alpha);
   r.w = bnback1(dh.w, z.w, c.sc.w, c.sh.w, c.c1.w, c.c2.w, c.c3.w, alpha);
+  return r;
+}
+
+// the same with the slope folded into the coefficient: dz = (u > 0 ? c1 : c1 alpha) dh + (c3 z + c2)
+__device__ __forceinline__ float bnback1_sel(float dh, float z, float sc, float sh, float c1, float c1a, float c2,
+                                             float c3) {
+  const float u = fmaf(z, sc, sh);
+  return fmaf(u > 0.f ? c1 : c1a, dh, fmaf(c3, z, c2));
+}
+__device__ __forceinline__ float4 bnback4_sel(float4 dh, float4 z, const BnBackCoef& c, float4 c1a) {
+  float4 r;
+  r.x = bnback1_sel(dh.x, z.x, c.sc.x, c.sh.x, c.c1.x, c1a.x, c.c2.x, c.c3.x);
+  r.y = bnback1_sel(dh.y, z.y, c.sc.y, c.sh.y, c.c1.y, c1a.y, c.c2.y, c.c3.y);
+  r.z = bnback1_sel(dh.z, z.z, c.sc.z, c.sh.z, c.c1.z, c1a.z, c.c2.z, c.c3.z);
+  r.w = bnback1_sel(dh.w, z.w, c.sc.w, c.sh.w, c.c1.w, c1a.w, c.c2.w, c.c3.w);
   return r;
 }
 

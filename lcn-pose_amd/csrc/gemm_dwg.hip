@@ -1,0 +1,251 @@
+// Weight-gradient GEMM, up to FOUR blocks of one output slab per workgroup
+// (gfx950).
+//
+// Same contract as gemm_dw_kernel (kernels_gemm.hip): dW_e(si, so) = A[:, si]^T .
+// dZ[:, so] over a workgroup's items of the batch, one partial slab per block
+// and slot.  Here a group is nb = 1..4 blocks (si_0.., so) and wave (ph, qh) =
+// (w >> 1, w & 1) owns the 32 x 32 sub-tile (rows 32ph.., columns 32qh..) of
+// EVERY block of the group (nb accumulators), so no wave idles whatever nb is,
+// and the staged D slab -- its two loads per thread, its BN-backward rebuild,
+// its transposed scatter -- serves up to four blocks instead of two: a 32-row
+// stage holds up to 64 MFMAs per wave between its two barriers, and an output
+// slab's dh / z rows are read by about half as many workgroups.  <= 168 VGPRs,
+// 49 KB of LDS: three workgroups per CU.
+#include "gemm_common.h"
+
+namespace lcn {
+
+constexpr int kDw4Ld = 36;
+
+template <bool PRO, bool DBB, bool DROP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void gemm_dwg_kernel(GemmDwArgs a) {
+  __shared__ __attribute__((aligned(16))) float Ds[64 * kDw4Ld];      // [q][row]
+  __shared__ __attribute__((aligned(16))) float As[4][64 * kDw4Ld];   // [p][row] per block
+  // channel constants: A (sc, sh) of the four input slabs; D sc, sh, c1, c2, c3
+  __shared__ __attribute__((aligned(16))) float tab[13 * 64];
+  const DwPlan pl = a.plan;
+  const int4 wgm = a.wgmap[blockIdx.x];
+  const int gi = __builtin_amdgcn_readfirstlane(wgm.x), slot = __builtin_amdgcn_readfirstlane(wgm.y);
+  const int item0 = __builtin_amdgcn_readfirstlane(wgm.z), n_it = __builtin_amdgcn_readfirstlane(wgm.w);
+  if (gi < 0) return;  // padding of the grid (uniform per workgroup)
+  // group: (so, nb, rank, count), (b0, b1, b2, b3) with -1 past nb
+  const int4 grp = a.groups[2 * gi], gb = a.groups[2 * gi + 1];
+  const int so = __builtin_amdgcn_readfirstlane(grp.x), nb = __builtin_amdgcn_readfirstlane(grp.y);
+  const int bq[4] = {__builtin_amdgcn_readfirstlane(gb.x), __builtin_amdgcn_readfirstlane(gb.y),
+                     __builtin_amdgcn_readfirstlane(gb.z), __builtin_amdgcn_readfirstlane(gb.w)};
+  int si[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) si[k] = __builtin_amdgcn_readfirstlane(a.blk[bq[k] >= 0 ? bq[k] : bq[0]].x);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(w);
+  const int lr = lane & 31, h = lane >> 5, ph = wv >> 1, qh = wv & 1;
+  const int wrank = __builtin_amdgcn_readfirstlane(grp.z), wcount = __builtin_amdgcn_readfirstlane(grp.w);
+  const bool may_write = DBB && a.dz_out != nullptr;
+  const int R = pl.item_rows, istride = pl.stride;
+
+  {
+    const int c = t & 63, k = t >> 6;  // 4 x 64 entries per pass
+    if constexpr (PRO) {
+      const int chk = ((k == 0 ? si[0] : k == 1 ? si[1] : k == 2 ? si[2] : si[3]) % a.spj_a) * kSlab + c;
+      tab[128 * k + c] = a.pro_scale[chk];
+      tab[128 * k + 64 + c] = a.pro_shift[chk];
+    }
+    if constexpr (DBB) {
+      const int ch = (so % a.spj_d) * kSlab + c, F = a.d_F;
+      tab[512 + t] = k == 0 ? a.d_scale[ch] : k == 1 ? a.d_shift[ch] : k == 2 ? a.d_c123[ch] : a.d_c123[F + ch];
+      if (k == 0) tab[768 + c] = a.d_c123[2 * F + ch];
+    }
+  }
+
+  f32x16 acc0, acc1, acc2, acc3;  // this wave's sub-tile of blocks 0..3
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { acc0[k] = 0.f; acc1[k] = 0.f; acc2[k] = 0.f; acc3[k] = 0.f; }
+  [[maybe_unused]] Dropout dr{};
+  if constexpr (DROP) dr = drop_resolve(a.d_drop);
+
+  // this thread's staging slots: the same four features f0 .. f0 + 3 of two
+  // rows, sr and sr + 16, of the stage's row tile
+  const int S_a = a.S_a, S_d = a.S_d;
+  const int sr = t & 15;
+  const int c40 = (t >> 5) * 64 + ((t >> 4) & 1) * 32 + sr, c41 = c40 + 16;
+  const int f0 = 8 * (t >> 5) + 4 * ((t >> 4) & 1);
+  float4 ra[4][2], rd0, rd1, rz0, rz1;
+  const int ntile = (a.B + kRT - 1) / kRT;
+  const __amdgpu_buffer_rsrc_t ares =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, (unsigned)ntile * S_a * 8192u, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dres =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.D, 0, (unsigned)ntile * S_d * 8192u, 0x00020000);
+  const __amdgpu_buffer_rsrc_t zres =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(DBB ? a.d_z : a.D), 0, (unsigned)ntile * S_d * 8192u, 0x00020000);
+  typedef float v4f_t __attribute__((ext_vector_type(4)));
+#define DW_BUFLD(RES, VOFF, SOFF)                                                      \
+  ({                                                                                   \
+    const v4f_t v_ = __builtin_bit_cast(v4f_t, __builtin_amdgcn_raw_buffer_load_b128((RES), (VOFF), (SOFF), 0)); \
+    make_float4(v_.x, v_.y, v_.z, v_.w);                                               \
+  })
+  const int v40 = c40 * 16, v41 = c41 * 16;
+#define DW_GLOAD(BASE)                                                     \
+  {                                                                        \
+    const int t_ = (BASE) / kRT;                                           \
+    const int od = (int)((unsigned)(t_ * S_d + so) * 8192u);               \
+    _Pragma("unroll") for (int k = 0; k < 4; ++k) {                        \
+      if (k < nb) {                                                 \
+        const int oa = (int)((unsigned)(t_ * S_a + si[k]) * 8192u);        \
+        ra[k][0] = DW_BUFLD(ares, v40, oa);                                \
+        ra[k][1] = DW_BUFLD(ares, v41, oa);                                \
+      }                                                                    \
+    }                                                                      \
+    rd0 = DW_BUFLD(dres, v40, od);                                         \
+    rd1 = DW_BUFLD(dres, v41, od);                                         \
+    if constexpr (DBB) {                                                   \
+      rz0 = DW_BUFLD(zres, v40, od);                                       \
+      rz1 = DW_BUFLD(zres, v41, od);                                       \
+    }                                                                      \
+  }
+  int it = 0, item = item0, base = item0 * R, iend = min(a.B, base + R);
+  bool more = n_it > 0 && base < a.B;
+  if (more) DW_GLOAD(base);
+  while (more) {
+    int nbase = base + kRT, nit = it, nitem = item, nend = iend;
+    if (nbase >= iend) {
+      nit = it + 1;
+      nitem = item + istride;
+      nbase = nitem * R;
+      nend = min(a.B, nbase + R);
+    }
+    const bool nmore = nit < n_it && nbase < a.B;
+    const int r1 = iend;
+    const bool writer = may_write && item % wcount == wrank;
+    __syncthreads();  // previous stage's fragment reads are done (and the tables written)
+    const bool v0 = base + sr < r1, v1 = base + sr + 16 < r1;
+    if constexpr (PRO) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k < nb) {
+          const float4 sc = *(const float4*)(tab + 128 * k + f0), sh = *(const float4*)(tab + 128 * k + 64 + f0);
+          ra[k][0] = bnact4(ra[k][0], sc, sh, a.alpha);
+          ra[k][1] = bnact4(ra[k][1], sc, sh, a.alpha);
+        }
+      }
+    }
+    if constexpr (DBB) {
+      BnBackCoef cf;
+      cf.sc = *(const float4*)(tab + 512 + f0); cf.sh = *(const float4*)(tab + 576 + f0);
+      cf.c1 = *(const float4*)(tab + 640 + f0); cf.c2 = *(const float4*)(tab + 704 + f0);
+      cf.c3 = *(const float4*)(tab + 768 + f0);
+      if constexpr (DROP) {  // tf.nn.dropout's gradient: dh * mask * scale
+        const int64_t row = base + sr;
+        const int col = so * kSlab + f0;
+        rd0.x = drop_apply(dr, row, col, rd0.x);
+        rd0.y = drop_apply(dr, row, col + 1, rd0.y);
+        rd0.z = drop_apply(dr, row, col + 2, rd0.z);
+        rd0.w = drop_apply(dr, row, col + 3, rd0.w);
+        rd1.x = drop_apply(dr, row + 16, col, rd1.x);
+        rd1.y = drop_apply(dr, row + 16, col + 1, rd1.y);
+        rd1.z = drop_apply(dr, row + 16, col + 2, rd1.z);
+        rd1.w = drop_apply(dr, row + 16, col + 3, rd1.w);
+      }
+      rd0 = bnback4(rd0, rz0, cf, a.alpha);
+      rd1 = bnback4(rd1, rz1, cf, a.alpha);
+      if (writer) {
+        float4* o = (float4*)a.dz_out;
+        const size_t t_ = base / kRT;
+        if (v0) o[(t_ * S_d + so) * 512 + c40] = rd0;
+        if (v1) o[(t_ * S_d + so) * 512 + c41] = rd1;
+      }
+    }
+    {  // rows past the item's end contribute nothing
+      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!v0) { ra[0][0] = z4; ra[1][0] = z4; ra[2][0] = z4; ra[3][0] = z4; rd0 = z4; }
+      if (!v1) { ra[0][1] = z4; ra[1][1] = z4; ra[2][1] = z4; ra[3][1] = z4; rd1 = z4; }
+    }
+    {
+      // transposed scatter: feature -> LDS row, batch row -> column
+#define DW_PUT(P, F4, OFF)             \
+  P[(OFF)] = (F4).x;                   \
+  P[(OFF) + kDw4Ld] = (F4).y;          \
+  P[(OFF) + 2 * kDw4Ld] = (F4).z;      \
+  P[(OFF) + 3 * kDw4Ld] = (F4).w;
+      const int o0 = f0 * kDw4Ld + sr, o1 = o0 + 16;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k < nb) { DW_PUT(As[k], ra[k][0], o0) DW_PUT(As[k], ra[k][1], o1) }
+      }
+      DW_PUT(Ds, rd0, o0) DW_PUT(Ds, rd1, o1)
+#undef DW_PUT
+    }
+    // the next stage's loads go out before the barrier (its wait hides part of
+    // their latency), and the MFMA phase runs at raised wave priority
+    if (nmore) DW_GLOAD(nbase);
+    __syncthreads();
+    __builtin_amdgcn_s_setprio(1);
+    {
+      const float* Dq = Ds + (32 * qh + lr) * kDw4Ld + 4 * h;
+      const float* Ap = &As[0][0] + (32 * ph + lr) * kDw4Ld + 4 * h;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 dv = *(const float4*)(Dq + 8 * g);
+        const float4 a0 = *(const float4*)(Ap + 8 * g);
+        float4 a1 = a0, a2 = a0, a3 = a0;
+        if (nb > 1) a1 = *(const float4*)(Ap + 64 * kDw4Ld + 8 * g);
+        if (nb > 2) a2 = *(const float4*)(Ap + 2 * 64 * kDw4Ld + 8 * g);
+        if (nb > 3) a3 = *(const float4*)(Ap + 3 * 64 * kDw4Ld + 8 * g);
+#define DWG_K(C)                                       \
+        acc0 = MFMA32(a0.C, dv.C, acc0);               \
+        if (nb > 1) acc1 = MFMA32(a1.C, dv.C, acc1);   \
+        if (nb > 2) acc2 = MFMA32(a2.C, dv.C, acc2);   \
+        if (nb > 3) acc3 = MFMA32(a3.C, dv.C, acc3);
+        DWG_K(x) DWG_K(y) DWG_K(z) DWG_K(w)
+#undef DWG_K
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    base = nbase;
+    it = nit;
+    item = nitem;
+    iend = nend;
+    more = nmore;
+  }
+#undef DW_GLOAD
+#undef DW_BUFLD
+  // this slot's partial of every block: this wave's sub-tile
+#define DWG_OUT(K, ACC)                                                        \
+  if (nb > (K)) {                                                              \
+    float* out = a.part + ((size_t)slot * a.nblk + bq[K]) * 4096 + 32 * qh;    \
+    _Pragma("unroll") for (int k = 0; k < 16; ++k) {                           \
+      const int p = 32 * ph + (k & 3) + 8 * (k >> 2) + 4 * h;                  \
+      out[p * 64 + lr] = ACC[k];                                               \
+    }                                                                          \
+  }
+  DWG_OUT(0, acc0) DWG_OUT(1, acc1) DWG_OUT(2, acc2) DWG_OUT(3, acc3)
+#undef DWG_OUT
+}
+
+int gemm_dwg_resident_slots() {
+  int dev = 0, per_cu = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm_dwg_kernel<true, true, false>, 256, 0) != hipSuccess)
+    return 0;
+  return per_cu * prop.multiProcessorCount;
+}
+
+void launch_gemm_dwg(const GemmDwArgs& a, hipStream_t s) {
+  const int grid = a.n_wg;
+  const bool pro = a.pro_scale != nullptr, dbb = a.d_bnback != 0;
+  const bool drop = dbb && a.d_drop.rate > 0.f;
+  if (pro && drop)
+    hipLaunchKernelGGL((gemm_dwg_kernel<true, true, true>), dim3(grid), dim3(256), 0, s, a);
+  else if (drop)
+    hipLaunchKernelGGL((gemm_dwg_kernel<false, true, true>), dim3(grid), dim3(256), 0, s, a);
+  else if (pro && dbb)
+    hipLaunchKernelGGL((gemm_dwg_kernel<true, true, false>), dim3(grid), dim3(256), 0, s, a);
+  else if (pro)
+    hipLaunchKernelGGL((gemm_dwg_kernel<true, false, false>), dim3(grid), dim3(256), 0, s, a);
+  else if (dbb)
+    hipLaunchKernelGGL((gemm_dwg_kernel<false, true, false>), dim3(grid), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_dwg_kernel<false, false, false>), dim3(grid), dim3(256), 0, s, a);
+}
+
+}  // namespace lcn

@@ -37,8 +37,9 @@ template <bool PRO, bool DBB, bool DROP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gemm_dw_kernel(GemmDwArgs a) {
   __shared__ __attribute__((aligned(16))) float Ds[64 * kDwLd];      // [q][row]
   __shared__ __attribute__((aligned(16))) float As[2][64 * kDwLd];   // [p][row] per block
-  // channel constants: A sc, sh of si0; A sc, sh of si1; D sc, sh, c1, c2, c3
-  __shared__ __attribute__((aligned(16))) float tab[9 * 64];
+  // channel constants: A sc, sh of si0; A sc, sh of si1 (both times (1 + alpha) / 2);
+  // D sc, sh, c1, c2, c3, c1 * alpha
+  __shared__ __attribute__((aligned(16))) float tab[10 * 64];
 #ifdef EXP_CLOCK
   const uint64_t ck0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -69,13 +70,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   {
     const int c = t & 63, k = t >> 6;  // 4 x 64 entries per pass
     if constexpr (PRO) {
+      // leaky(u) = max(u, alpha u) = a u + b |u| with a = (1 + alpha) / 2, b = (1 - alpha) / 2: with the
+      // tables scaled by a, the operand is u' + (b / a) |u'|, two operations an element instead of three
+      // (within 2 ulp of the max form; the operand of the weight gradient only)
       const int ch0 = (si0 % a.spj_a) * kSlab + c, ch1 = (si1 % a.spj_a) * kSlab + c;
-      tab[t] = k == 0 ? a.pro_scale[ch0] : k == 1 ? a.pro_shift[ch0] : k == 2 ? a.pro_scale[ch1] : a.pro_shift[ch1];
+      tab[t] = 0.5f * (1.f + a.alpha) *
+               (k == 0 ? a.pro_scale[ch0] : k == 1 ? a.pro_shift[ch0] : k == 2 ? a.pro_scale[ch1] : a.pro_shift[ch1]);
     }
     if constexpr (DBB) {
       const int ch = (so % a.spj_d) * kSlab + c, F = a.d_F;
       tab[256 + t] = k == 0 ? a.d_scale[ch] : k == 1 ? a.d_shift[ch] : k == 2 ? a.d_c123[ch] : a.d_c123[F + ch];
       if (k == 0) tab[512 + c] = a.d_c123[2 * F + ch];
+      if (k == 1) tab[576 + c] = a.d_c123[ch] * a.alpha;
     }
   }
 
@@ -164,13 +170,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
     const bool v0 = base + sr < r1, v1 = base + sr + 16 < r1;
 #ifndef EXP_DW_NOSTAGE  // diagnostic build without the staging phase (loads, transforms, scatter)
     if constexpr (PRO) {
+      const float ba = (1.f - a.alpha) / (1.f + a.alpha);
       const float4 sc0 = *(const float4*)(tab + f0), sh0 = *(const float4*)(tab + 64 + f0);
-      ra0 = bnact4(ra0, sc0, sh0, a.alpha);
-      ra1 = bnact4(ra1, sc0, sh0, a.alpha);
+      ra0 = bnact4_scaled(ra0, sc0, sh0, ba);
+      ra1 = bnact4_scaled(ra1, sc0, sh0, ba);
       if (two) {
         const float4 sc1 = *(const float4*)(tab + 128 + f0), sh1 = *(const float4*)(tab + 192 + f0);
-        rb0 = bnact4(rb0, sc1, sh1, a.alpha);
-        rb1 = bnact4(rb1, sc1, sh1, a.alpha);
+        rb0 = bnact4_scaled(rb0, sc1, sh1, ba);
+        rb1 = bnact4_scaled(rb1, sc1, sh1, ba);
       }
     }
     if constexpr (DBB) {
@@ -178,6 +185,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
       cf.sc = *(const float4*)(tab + 256 + f0); cf.sh = *(const float4*)(tab + 320 + f0);
       cf.c1 = *(const float4*)(tab + 384 + f0); cf.c2 = *(const float4*)(tab + 448 + f0);
       cf.c3 = *(const float4*)(tab + 512 + f0);
+      const float4 c1a = *(const float4*)(tab + 576 + f0);
       if constexpr (DROP) {  // tf.nn.dropout's gradient: dh * mask * scale
         const int64_t row = base + sr;
         const int col = so * kSlab + f0;
@@ -190,8 +198,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
         rd1.z = drop_apply(dr, row + 16, col + 2, rd1.z);
         rd1.w = drop_apply(dr, row + 16, col + 3, rd1.w);
       }
-      rd0 = bnback4(rd0, rz0, cf, a.alpha);
-      rd1 = bnback4(rd1, rz1, cf, a.alpha);
+      rd0 = bnback4_sel(rd0, rz0, cf, c1a);
+      rd1 = bnback4_sel(rd1, rz1, cf, c1a);
       if (writer) {
         float4* o = (float4*)a.dz_out;
         const int t_ = base / kRT;

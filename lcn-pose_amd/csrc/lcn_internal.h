@@ -361,6 +361,22 @@ struct GemmDwArgs {
 void launch_gemm_dw(const GemmDwArgs& a, hipStream_t s);
 // workgroups of the weight-gradient kernel the current device holds at once
 int gemm_dw_resident_slots();
+// up to four blocks of an output slab per workgroup (gemm_dwg.hip): two int4
+// per group, (so, blocks, rank, count) and (b0, b1, b2, b3) with -1 past the
+// group's blocks
+void launch_gemm_dwg(const GemmDwArgs& a, hipStream_t s);
+int gemm_dwg_resident_slots();
+// the groups of an output slab that holds d blocks: fours first, without
+// leaving a single block over (5 -> 3 + 2, 9 -> 4 + 3 + 2); 1 -> 1
+inline std::vector<int> dwg_group_sizes(int d) {
+  std::vector<int> g;
+  while (d > 0) {
+    const int n = d >= 8 || d == 4 || d == 6 || d == 7 ? 4 : d == 5 ? 3 : d;  // d <= 3: the rest
+    g.push_back(n);
+    d -= n;
+  }
+  return g;
+}
 // sum partials over chunks; write into dense dW [rows][ld] at (si*64+p, so*64+q),
 // dropping rows >= rows_valid / columns >= cols_valid (padding of thin layers)
 void launch_dw_reduce(const float* part, int nchunks, int nblk, const int2* blk,

@@ -20,6 +20,10 @@
 //           output slabs multiply the same input slab), the weight DMA on every one
 //   mode 10 mode 9's register shape (two accumulator pairs, alternating) with
 //           the activation loads on every iteration: the control for mode 9
+//   mode 11 the weight-gradient kernel's MFMA phase alone: per iteration two
+//           barriers, 12 ds_read_b128 of transposed fragments (row stride 36
+//           floats) and 32 MFMAs on two accumulators, no global loads
+//   mode 12 mode 11 with one barrier per iteration; mode 13 with none
 // 4 workgroups of 4 waves per CU as in the GEMM.  Results are meaningless; only
 // the rate matters.
 //   hipcc --offload-arch=gfx950 -O3 -o mfma_steps mfma_steps.hip && ./mfma_steps
@@ -157,6 +161,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
     }
   };
+  if (MODE >= 11 && MODE <= 13) {
+    const float* L = (const float*)Wl;  // As[2][64 * 36], Ds[64 * 36] floats: 27 KB of the 32 KB
+    const int lr = lane & 31, h = lane >> 5, bi = w >> 1, hp = w & 1;
+    const float* Ap = L + bi * 2304 + (32 * hp + lr) * 36 + 4 * h;
+    const float* D0 = L + 4608 + lr * 36 + 4 * h;
+    const float* D1 = L + 4608 + (32 + lr) * 36 + 4 * h;
+    for (int it = 0; it < iters; ++it) {
+      if (MODE <= 12) __syncthreads();
+      if (MODE == 11) __syncthreads();
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 av = *(const float4*)(Ap + 8 * g);
+        const float4 d0 = *(const float4*)(D0 + 8 * g);
+        const float4 d1 = *(const float4*)(D1 + 8 * g);
+        acc0 = MFMA32(av.x, d0.x, acc0); acc1 = MFMA32(av.x, d1.x, acc1);
+        acc0 = MFMA32(av.y, d0.y, acc0); acc1 = MFMA32(av.y, d1.y, acc1);
+        acc0 = MFMA32(av.z, d0.z, acc0); acc1 = MFMA32(av.z, d1.z, acc1);
+        acc0 = MFMA32(av.w, d0.w, acc0); acc1 = MFMA32(av.w, d1.w, acc1);
+      }
+    }
+  } else
   if (MODE == 9 || MODE == 10) {
     // iterations come in fours: (xa, slab 0) (xa, slab 1) (xb, slab 0) (xb, slab 1)
     for (int it = 0; it < iters; it += 4) {
@@ -213,7 +238,7 @@ static void run(int iters, const float4* X, const float4* W, int n_tiles, float*
     (void)hipEventElapsedTime(&ms, e0, e1);
     best = ms < best ? ms : best;
   }
-  const double flop = (double)grid * 4 * iters * 64 * 4096.0;
+  const double flop = (double)grid * 4 * iters * (MODE >= 11 && MODE <= 13 ? 32 : 64) * 4096.0;
   std::printf("mode %d (%d workgroups per CU): %.2f ms, %.1f TFLOP/s (%.1f%% of 157.3)\n", MODE, WPE, best, flop / (best * 1e-3) / 1e12,
               100.0 * flop / (best * 1e-3) / 1e12 / 157.3);
 }
@@ -242,6 +267,11 @@ int main(int argc, char** argv) {
   run<8>(iters, X, W, n_tiles, out, grid);
   run<7, 3>(iters, X, W, n_tiles, out, grid);
   run<8, 3>(iters, X, W, n_tiles, out, grid);
+  run<11>(iters, X, W, n_tiles, out, grid);
+  run<12>(iters, X, W, n_tiles, out, grid);
+  run<13>(iters, X, W, n_tiles, out, grid);
+  run<11, 3>(iters, X, W, n_tiles, out, grid);
+  run<11, 5>(iters, X, W, n_tiles, out, grid);
   run<9, 3>(iters, X, W, n_tiles, out, grid);
   run<10, 3>(iters, X, W, n_tiles, out, grid);
   run<9, 2>(iters, X, W, n_tiles, out, grid);
