@@ -3,34 +3,42 @@
 //
 // Same contract as gemm_dw_kernel (kernels_gemm.hip): dW_e(si, so) = A[:, si]^T .
 // dZ[:, so] over a workgroup's items of the batch, one partial slab per block
-// and slot.  Here a group is nb = 1..4 blocks (si_0.., so) and wave (ph, qh) =
-// (w >> 1, w & 1) owns the 32 x 32 sub-tile (rows 32ph.., columns 32qh..) of
-// EVERY block of the group (nb accumulators), so no wave idles whatever nb is,
-// and the staged D slab -- its two loads per thread, its BN-backward rebuild,
+// and slot.  Here a group is 1..4 blocks (si_0.., so) -- dwg_body has the two
+// wave-to-tile maps -- and the staged D slab -- its two loads per thread, its BN-backward rebuild,
 // its transposed scatter -- serves up to four blocks instead of two: a 32-row
 // stage holds up to 64 MFMAs per wave between its two barriers, and an output
 // slab's dh / z rows are read by about half as many workgroups.  <= 168 VGPRs,
 // 49 KB of LDS: three workgroups per CU.
+//
+// Measured in gemm_bench only (B = 65 536, knn 3, one box per comparison; raw /
+// BN-backward D / + BN-apply A, % of the fp32 MFMA peak, kernel alone):
+//   * the 37 complete quads (148 of 175 blocks), a whole block per wave:
+//     80.6 / 77.3 / 73.0 % against 80.0 / 72.5 / 68.7 % for the two-block kernel
+//     over all blocks; with the sub-tile map instead 76.3 / 73.4 / 71.8 %;
+//   * all 175 blocks in one launch (fours, then the remainder of an output slab
+//     as one group of 1..3: 37 + 17 groups): 774 / 845 / 1139 us against 753 /
+//     853 / 885 us -- the remainders (the output slabs hold 5..17 blocks) run
+//     slower at three workgroups per CU than they do now at four, and the
+//     BN-apply x BN-backward instance spills (27 registers) beside its 64
+//     accumulator and 48 staging registers.
+// Not part of liblcn.
 #include "gemm_common.h"
 
 namespace lcn {
 
 constexpr int kDw4Ld = 36;
 
-template <bool PRO, bool DBB, bool DROP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void gemm_dwg_kernel(GemmDwArgs a) {
-  __shared__ __attribute__((aligned(16))) float Ds[64 * kDw4Ld];      // [q][row]
-  __shared__ __attribute__((aligned(16))) float As[4][64 * kDw4Ld];   // [p][row] per block
-  // channel constants: A (sc, sh) of the four input slabs; D sc, sh, c1, c2, c3
-  __shared__ __attribute__((aligned(16))) float tab[13 * 64];
+// The whole workgroup for one group shape.  QUAD (four blocks): wave w owns
+// block w whole, four accumulators = (rows 0..31 | 32..63) x (columns 0..31 |
+// 32..63), four fragment reads per 16 MFMAs.  Otherwise (1..3 blocks): wave
+// (ph, qh) owns the 32 x 32 sub-tile (rows 32ph.., columns 32qh..) of every block
+// of the group, one accumulator a block, so no wave idles.
+template <bool PRO, bool DBB, bool DROP, bool QUAD>
+__device__ __forceinline__ void dwg_body(const GemmDwArgs& a, float* Ds, float (*As)[64 * kDw4Ld], float* tab, int gi,
+                                         int slot, int item0, int n_it, const int4 grp, const int4 gb) {
   const DwPlan pl = a.plan;
-  const int4 wgm = a.wgmap[blockIdx.x];
-  const int gi = __builtin_amdgcn_readfirstlane(wgm.x), slot = __builtin_amdgcn_readfirstlane(wgm.y);
-  const int item0 = __builtin_amdgcn_readfirstlane(wgm.z), n_it = __builtin_amdgcn_readfirstlane(wgm.w);
-  if (gi < 0) return;  // padding of the grid (uniform per workgroup)
-  // group: (so, nb, rank, count), (b0, b1, b2, b3) with -1 past nb
-  const int4 grp = a.groups[2 * gi], gb = a.groups[2 * gi + 1];
-  const int so = __builtin_amdgcn_readfirstlane(grp.x), nb = __builtin_amdgcn_readfirstlane(grp.y);
+  const int so = __builtin_amdgcn_readfirstlane(grp.x);
+  const int nb = QUAD ? 4 : __builtin_amdgcn_readfirstlane(grp.y);
   const int bq[4] = {__builtin_amdgcn_readfirstlane(gb.x), __builtin_amdgcn_readfirstlane(gb.y),
                      __builtin_amdgcn_readfirstlane(gb.z), __builtin_amdgcn_readfirstlane(gb.w)};
   int si[4];
@@ -47,13 +55,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     const int c = t & 63, k = t >> 6;  // 4 x 64 entries per pass
     if constexpr (PRO) {
       const int chk = ((k == 0 ? si[0] : k == 1 ? si[1] : k == 2 ? si[2] : si[3]) % a.spj_a) * kSlab + c;
-      tab[128 * k + c] = a.pro_scale[chk];
-      tab[128 * k + 64 + c] = a.pro_shift[chk];
+      // leaky(u) = u' + ((1 - alpha) / (1 + alpha)) |u'| for u' = u (1 + alpha) / 2: tables pre-scaled
+      tab[128 * k + c] = 0.5f * (1.f + a.alpha) * a.pro_scale[chk];
+      tab[128 * k + 64 + c] = 0.5f * (1.f + a.alpha) * a.pro_shift[chk];
     }
     if constexpr (DBB) {
       const int ch = (so % a.spj_d) * kSlab + c, F = a.d_F;
       tab[512 + t] = k == 0 ? a.d_scale[ch] : k == 1 ? a.d_shift[ch] : k == 2 ? a.d_c123[ch] : a.d_c123[F + ch];
       if (k == 0) tab[768 + c] = a.d_c123[2 * F + ch];
+      if (k == 1) tab[832 + c] = a.d_c123[ch] * a.alpha;
     }
   }
 
@@ -119,12 +129,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     __syncthreads();  // previous stage's fragment reads are done (and the tables written)
     const bool v0 = base + sr < r1, v1 = base + sr + 16 < r1;
     if constexpr (PRO) {
+      const float ba = (1.f - a.alpha) / (1.f + a.alpha);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if (k < nb) {
           const float4 sc = *(const float4*)(tab + 128 * k + f0), sh = *(const float4*)(tab + 128 * k + 64 + f0);
-          ra[k][0] = bnact4(ra[k][0], sc, sh, a.alpha);
-          ra[k][1] = bnact4(ra[k][1], sc, sh, a.alpha);
+          ra[k][0] = bnact4_scaled(ra[k][0], sc, sh, ba);
+          ra[k][1] = bnact4_scaled(ra[k][1], sc, sh, ba);
         }
       }
     }
@@ -133,6 +144,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       cf.sc = *(const float4*)(tab + 512 + f0); cf.sh = *(const float4*)(tab + 576 + f0);
       cf.c1 = *(const float4*)(tab + 640 + f0); cf.c2 = *(const float4*)(tab + 704 + f0);
       cf.c3 = *(const float4*)(tab + 768 + f0);
+      const float4 c1a = *(const float4*)(tab + 832 + f0);
       if constexpr (DROP) {  // tf.nn.dropout's gradient: dh * mask * scale
         const int64_t row = base + sr;
         const int col = so * kSlab + f0;
@@ -145,8 +157,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         rd1.z = drop_apply(dr, row + 16, col + 2, rd1.z);
         rd1.w = drop_apply(dr, row + 16, col + 3, rd1.w);
       }
-      rd0 = bnback4(rd0, rz0, cf, a.alpha);
-      rd1 = bnback4(rd1, rz1, cf, a.alpha);
+      rd0 = bnback4_sel(rd0, rz0, cf, c1a);
+      rd1 = bnback4_sel(rd1, rz1, cf, c1a);
       if (writer) {
         float4* o = (float4*)a.dz_out;
         const size_t t_ = base / kRT;
@@ -179,22 +191,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     if (nmore) DW_GLOAD(nbase);
     __syncthreads();
     __builtin_amdgcn_s_setprio(1);
-    {
+    if constexpr (QUAD) {
+      const float* A0 = As[wv] + lr * kDw4Ld + 4 * h;
+      const float* A1 = As[wv] + (32 + lr) * kDw4Ld + 4 * h;
+      const float* D0 = Ds + lr * kDw4Ld + 4 * h;
+      const float* D1 = Ds + (32 + lr) * kDw4Ld + 4 * h;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 a0 = *(const float4*)(A0 + 8 * g), a1 = *(const float4*)(A1 + 8 * g);
+        const float4 d0 = *(const float4*)(D0 + 8 * g), d1 = *(const float4*)(D1 + 8 * g);
+#define DWG_Q(C)                                                                \
+        acc0 = MFMA32(a0.C, d0.C, acc0); acc1 = MFMA32(a0.C, d1.C, acc1);       \
+        acc2 = MFMA32(a1.C, d0.C, acc2); acc3 = MFMA32(a1.C, d1.C, acc3);
+        DWG_Q(x) DWG_Q(y) DWG_Q(z) DWG_Q(w)
+#undef DWG_Q
+      }
+    } else {
       const float* Dq = Ds + (32 * qh + lr) * kDw4Ld + 4 * h;
       const float* Ap = &As[0][0] + (32 * ph + lr) * kDw4Ld + 4 * h;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 dv = *(const float4*)(Dq + 8 * g);
         const float4 a0 = *(const float4*)(Ap + 8 * g);
-        float4 a1 = a0, a2 = a0, a3 = a0;
+        float4 a1 = a0, a2 = a0;
         if (nb > 1) a1 = *(const float4*)(Ap + 64 * kDw4Ld + 8 * g);
         if (nb > 2) a2 = *(const float4*)(Ap + 2 * 64 * kDw4Ld + 8 * g);
-        if (nb > 3) a3 = *(const float4*)(Ap + 3 * 64 * kDw4Ld + 8 * g);
 #define DWG_K(C)                                       \
         acc0 = MFMA32(a0.C, dv.C, acc0);               \
         if (nb > 1) acc1 = MFMA32(a1.C, dv.C, acc1);   \
-        if (nb > 2) acc2 = MFMA32(a2.C, dv.C, acc2);   \
-        if (nb > 3) acc3 = MFMA32(a3.C, dv.C, acc3);
+        if (nb > 2) acc2 = MFMA32(a2.C, dv.C, acc2);
         DWG_K(x) DWG_K(y) DWG_K(z) DWG_K(w)
 #undef DWG_K
       }
@@ -208,7 +233,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   }
 #undef DW_GLOAD
 #undef DW_BUFLD
-  // this slot's partial of every block: this wave's sub-tile
+  if constexpr (QUAD) {  // this slot's partial of this wave's block
+    const int myblk = wv == 0 ? bq[0] : wv == 1 ? bq[1] : wv == 2 ? bq[2] : bq[3];
+    float* out = a.part + ((size_t)slot * a.nblk + myblk) * 4096;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int p = (k & 3) + 8 * (k >> 2) + 4 * h;
+      out[p * 64 + lr] = acc0[k];
+      out[p * 64 + 32 + lr] = acc1[k];
+      out[(32 + p) * 64 + lr] = acc2[k];
+      out[(32 + p) * 64 + 32 + lr] = acc3[k];
+    }
+  } else {  // this slot's partial of every block: this wave's sub-tile
 #define DWG_OUT(K, ACC)                                                        \
   if (nb > (K)) {                                                              \
     float* out = a.part + ((size_t)slot * a.nblk + bq[K]) * 4096 + 32 * qh;    \
@@ -217,8 +253,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       out[p * 64 + lr] = ACC[k];                                               \
     }                                                                          \
   }
-  DWG_OUT(0, acc0) DWG_OUT(1, acc1) DWG_OUT(2, acc2) DWG_OUT(3, acc3)
+    DWG_OUT(0, acc0) DWG_OUT(1, acc1) DWG_OUT(2, acc2)
 #undef DWG_OUT
+  }
+}
+
+template <bool PRO, bool DBB, bool DROP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void gemm_dwg_kernel(GemmDwArgs a) {
+  __shared__ __attribute__((aligned(16))) float Ds[64 * kDw4Ld];      // [q][row]
+  __shared__ __attribute__((aligned(16))) float As[4][64 * kDw4Ld];   // [p][row] per block
+  // channel constants: A (sc, sh) of the four input slabs; D sc, sh, c1, c2, c3, c1 * alpha
+  __shared__ __attribute__((aligned(16))) float tab[14 * 64];
+  const int4 wgm = a.wgmap[blockIdx.x];
+  const int gi = __builtin_amdgcn_readfirstlane(wgm.x), slot = __builtin_amdgcn_readfirstlane(wgm.y);
+  const int item0 = __builtin_amdgcn_readfirstlane(wgm.z), n_it = __builtin_amdgcn_readfirstlane(wgm.w);
+  if (gi < 0) return;  // padding of the grid (uniform per workgroup)
+  // group: (so, blocks, rank, count), (b0, b1, b2, b3) with -1 past the group's blocks
+  const int4 grp = a.groups[2 * gi], gb = a.groups[2 * gi + 1];
+  if (__builtin_amdgcn_readfirstlane(grp.y) == 4)
+    dwg_body<PRO, DBB, DROP, true>(a, Ds, As, tab, gi, slot, item0, n_it, grp, gb);
+  else
+    dwg_body<PRO, DBB, DROP, false>(a, Ds, As, tab, gi, slot, item0, n_it, grp, gb);
 }
 
 int gemm_dwg_resident_slots() {

@@ -366,15 +366,10 @@ int gemm_dw_resident_slots();
 // group's blocks
 void launch_gemm_dwg(const GemmDwArgs& a, hipStream_t s);
 int gemm_dwg_resident_slots();
-// the groups of an output slab that holds d blocks: fours first, without
-// leaving a single block over (5 -> 3 + 2, 9 -> 4 + 3 + 2); 1 -> 1
+// the groups of an output slab that holds d blocks: fours, then the rest (1..3) as one group
 inline std::vector<int> dwg_group_sizes(int d) {
-  std::vector<int> g;
-  while (d > 0) {
-    const int n = d >= 8 || d == 4 || d == 6 || d == 7 ? 4 : d == 5 ? 3 : d;  // d <= 3: the rest
-    g.push_back(n);
-    d -= n;
-  }
+  std::vector<int> g(d / 4, 4);
+  if (d % 4) g.push_back(d % 4);
   return g;
 }
 // sum partials over chunks; write into dense dW [rows][ld] at (si*64+p, so*64+q),
