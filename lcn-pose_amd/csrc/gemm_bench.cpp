@@ -221,7 +221,22 @@ int main(int argc, char** argv) {
     d.plan = make_dw_plan(B, (int)grp.size(), slots, nch, 128);
     if (std::getenv("LCN_DW_ITEM")) d.plan.item_rows = std::atoi(std::getenv("LCN_DW_ITEM"));
     if (std::getenv("LCN_DW_ROUNDS") && d.plan.stride == 8) d.plan.n_slots = 8 * d.plan.sub * std::atoi(std::getenv("LCN_DW_ROUNDS"));
-    const std::vector<int4> map = make_dw_wgmap((int)grp.size(), d.plan, B);
+    std::vector<int4> map = make_dw_wgmap((int)grp.size(), d.plan, B);
+    if (std::getenv("LCN_DW_EQROUNDS") && d.plan.stride == 8) {  // experiment: rounds of equal size (batch segments)
+      const int rounds = std::atoi(std::getenv("LCN_DW_EQROUNDS")), groups = (int)grp.size();
+      const int n_items = (int)((B + d.plan.item_rows - 1) / d.plan.item_rows);
+      d.plan.sub = 1;
+      d.plan.n_slots = 8 * rounds;
+      map.assign((size_t)8 * rounds * groups, make_int4(-1, 0, 0, 0));
+      for (int x = 0; x < 8; ++x) {
+        const int n = n_items > x ? (n_items - x + 7) / 8 : 0;
+        for (int r = 0; r < rounds; ++r) {
+          const int lo = (int)((int64_t)n * r / rounds), hi = (int)((int64_t)n * (r + 1) / rounds);
+          for (int g = 0; g < groups; ++g)
+            map[8 * ((size_t)r * groups + g) + x] = make_int4(g, 8 * r + x, x + 8 * lo, hi - lo);
+        }
+      }
+    }
     dw_map_host = map;
     d.wgmap = dev(map);
     d.n_wg = (int)map.size();

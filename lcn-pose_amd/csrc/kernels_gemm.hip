@@ -124,11 +124,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   const __amdgpu_buffer_rsrc_t zres = __builtin_amdgcn_make_buffer_rsrc(
       (void*)((const char*)(DBB ? a.d_z : a.D) + (size_t)tile0 * S_d * 8192), 0, (unsigned)ntile * S_d * 8192u, 0x00020000);
   typedef float v4f_t __attribute__((ext_vector_type(4)));
-#define DW_BUFLD(RES, VOFF, SOFF)                                                      \
+#define DW_BUFLDX(RES, VOFF, SOFF, AUX)                                                \
   ({                                                                                   \
-    const v4f_t v_ = __builtin_bit_cast(v4f_t, __builtin_amdgcn_raw_buffer_load_b128((RES), (VOFF), (SOFF), 0)); \
+    const v4f_t v_ = __builtin_bit_cast(v4f_t, __builtin_amdgcn_raw_buffer_load_b128((RES), (VOFF), (SOFF), (AUX))); \
     make_float4(v_.x, v_.y, v_.z, v_.w);                                               \
   })
+  // diagnostic builds: cache policy bits (2 = nt) of the A / D,z loads
+#ifndef EXP_DW_AUX_A
+#define EXP_DW_AUX_A 0
+#endif
+#ifndef EXP_DW_AUX_D
+#define EXP_DW_AUX_D 0
+#endif
+#define DW_BUFLD(RES, VOFF, SOFF) DW_BUFLDX(RES, VOFF, SOFF, EXP_DW_AUX_A)
+#define DW_BUFLDD(RES, VOFF, SOFF) DW_BUFLDX(RES, VOFF, SOFF, EXP_DW_AUX_D)
   const int v40 = c40 * 16, v41 = c41 * 16;
 #define DW_GLOAD(BASE)                                                     \
   {                                                                        \
@@ -141,11 +150,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
       rb0 = DW_BUFLD(ares, v40, oa1);                                      \
       rb1 = DW_BUFLD(ares, v41, oa1);                                      \
     }                                                                      \
-    rd0 = DW_BUFLD(dres, v40, od);                                         \
-    rd1 = DW_BUFLD(dres, v41, od);                                         \
+    rd0 = DW_BUFLDD(dres, v40, od);                                        \
+    rd1 = DW_BUFLDD(dres, v41, od);                                        \
     if constexpr (DBB) {                                                   \
-      rz0 = DW_BUFLD(zres, v40, od);                                       \
-      rz1 = DW_BUFLD(zres, v41, od);                                       \
+      rz0 = DW_BUFLDD(zres, v40, od);                                      \
+      rz1 = DW_BUFLDD(zres, v41, od);                                      \
     }                                                                      \
   }
   // stages of this workgroup: its items, 32 rows a stage; the next stage's rows
@@ -297,6 +306,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   }
 #undef DW_GLOAD
 #undef DW_BUFLD
+#undef DW_BUFLDD
+#undef DW_BUFLDX
 #undef DW_TILE
 #undef DW_IX
 #ifdef EXP_CLOCK
