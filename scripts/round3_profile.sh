@@ -1,8 +1,8 @@
 #!/bin/bash
-# On the GPU box: the round's evidence besides scripts/round_profile.sh --
+# On the GPU box: the measured lines besides scripts/round_profile.sh --
 # cfg2 / cfg4 / cfg5 lines, the per-GPU shard sizes of a strong-scaling cfg3
 # run, the reference's small batches, a one-rank RCCL run.  Results under
-# gpurun_out/r3/ (copy what is to be judged into profiles/).
+# gpurun_out/r3/ (copy what is to be kept into profiles/).
 R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out/r3
 mkdir -p $O

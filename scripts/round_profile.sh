@@ -1,7 +1,7 @@
 #!/bin/bash
-# On the GPU box: the round's evidence in one go -- GPU tests, bench line,
+# On the GPU box: the measured evidence in one go -- GPU tests, bench line,
 # rocprofv3 kernel stats + trace of the same bench command, PMC traffic.
-# Results under gpurun_out/round/ (copy what is to be judged into profiles/).
+# Results under gpurun_out/round/ (copy what is to be kept into profiles/).
 R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out/round
 mkdir -p $O
