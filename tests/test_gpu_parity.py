@@ -20,6 +20,8 @@ CASES = [
     ("lc_knn2_L3", dict(F=64, L=3, knn=2), 300),
     ("lc_knn5_L1", dict(F=64, L=1, knn=5), 64),
     ("exp_L2_F128", dict(F=128, L=2, knn=2, mask="exponential"), 96),
+    # three slabs per joint: two pair up, the third finds its partner across joints
+    ("lc_F192_knn4", dict(F=192, L=1, knn=4), 70),
     ("lc_inF3", dict(F=64, L=1, knn=3, in_F=3), 160),
     ("lc_nores", dict(F=64, L=2, knn=3, residual=False), 128),
     ("lc_nobn", dict(F=64, L=1, knn=2, batch_norm=False), 128),
