@@ -4,6 +4,8 @@
 // thin lift / output layers).  The batch is split into chunks; each chunk
 // writes a partial slab that dw_reduce sums in a fixed order (deterministic,
 // no atomics).
+#include <cstdlib>
+
 #include "gemm_common.h"
 
 namespace lcn {
@@ -351,21 +353,26 @@ int gemm_dw_resident_slots() {
 
 void launch_gemm_dw(const GemmDwArgs& a, hipStream_t s) {
   const int grid = a.n_wg;
+#ifdef EXP_DW_LDSPAD  // diagnostic build: unused dynamic LDS per workgroup (bytes), to lower the residency
+  const size_t pad = std::getenv("LCN_DW_LDSPAD") ? (size_t)std::atoi(std::getenv("LCN_DW_LDSPAD")) : 0;
+#else
+  const size_t pad = 0;
+#endif
   const bool pro = a.pro_scale != nullptr, dbb = a.d_bnback != 0;
   // the dropout variants are separate instances: the mask hash costs registers
   const bool drop = dbb && a.d_drop.rate > 0.f;
   if (pro && drop)
-    hipLaunchKernelGGL((gemm_dw_kernel<true, true, true>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw_kernel<true, true, true>), dim3(grid), dim3(256), pad, s, a);
   else if (drop)
-    hipLaunchKernelGGL((gemm_dw_kernel<false, true, true>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw_kernel<false, true, true>), dim3(grid), dim3(256), pad, s, a);
   else if (pro && dbb)
-    hipLaunchKernelGGL((gemm_dw_kernel<true, true, false>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw_kernel<true, true, false>), dim3(grid), dim3(256), pad, s, a);
   else if (pro)
-    hipLaunchKernelGGL((gemm_dw_kernel<true, false, false>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw_kernel<true, false, false>), dim3(grid), dim3(256), pad, s, a);
   else if (dbb)
-    hipLaunchKernelGGL((gemm_dw_kernel<false, true, false>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw_kernel<false, true, false>), dim3(grid), dim3(256), pad, s, a);
   else
-    hipLaunchKernelGGL((gemm_dw_kernel<false, false, false>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw_kernel<false, false, false>), dim3(grid), dim3(256), pad, s, a);
 }
 
 // Sum the chunk partials of every block in a fixed order and scatter into the
