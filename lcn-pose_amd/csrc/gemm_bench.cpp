@@ -244,81 +244,32 @@ int main(int argc, char** argv) {
                 d.plan.item_rows, d.plan.stride, d.plan.n_slots, d.n_wg, slots);
   }
   d.part = part;
-  // up to four blocks per workgroup (gemm_dwg.hip), all blocks
+  // four blocks per workgroup (gemm_dw4.hip): the complete quads of every output slab
   GemmDwArgs d4 = d;
-  int nblk4 = nblk;
+  int nblk4 = 0;
   {
-    struct G { int so, nb, rank, count, b[4]; };
-    std::vector<G> gs;
+    std::vector<int4> g4;
     for (int so = 0; so < J; ++so) {
       std::vector<int> ids;
       for (int b = 0; b < nblk; ++b)
         if (blk[b].y == so) ids.push_back(b);
-      const std::vector<int> sz = dwg_group_sizes((int)ids.size());
-      int at = 0;
-      for (size_t q = 0; q < sz.size(); ++q) {
-        G g{so, sz[q], (int)q, (int)sz.size(), {-1, -1, -1, -1}};
-        for (int k = 0; k < sz[q]; ++k) g.b[k] = ids[at++];
-        gs.push_back(g);
+      const int count = (int)ids.size() / 4;
+      for (int q = 0; q < count; ++q) {
+        g4.push_back(make_int4(so, 4, q, count));
+        g4.push_back(make_int4(ids[4 * q], ids[4 * q + 1], ids[4 * q + 2], ids[4 * q + 3]));
+        nblk4 += 4;
       }
     }
-    std::stable_sort(gs.begin(), gs.end(), [](const G& x, const G& y) { return x.nb > y.nb; });  // long groups first
-    if (std::getenv("LCN_DWG_ONLY")) {  // timing only: the groups of one size
-      const int only = std::atoi(std::getenv("LCN_DWG_ONLY"));
-      std::vector<G> keep;
-      for (const G& g : gs) if (g.nb == only) keep.push_back(g);
-      gs.swap(keep);
-      nblk4 = only * (int)gs.size();
-    }
-    std::vector<int4> g4;
-    for (const G& g : gs) {
-      g4.push_back(make_int4(g.so, g.nb, g.rank, g.count));
-      g4.push_back(make_int4(g.b[0], g.b[1], g.b[2], g.b[3]));
-    }
     d4.groups = dev(g4);
-    d4.ngroups = (int)gs.size();
-    const int slots4 = std::getenv("LCN_DW_SLOTS") ? std::atoi(std::getenv("LCN_DW_SLOTS")) : gemm_dwg_resident_slots();
+    d4.ngroups = (int)g4.size() / 2;
+    const int slots4 = std::getenv("LCN_DW_SLOTS") ? std::atoi(std::getenv("LCN_DW_SLOTS")) : gemm_dw4_resident_slots();
     d4.plan = make_dw_plan(B, d4.ngroups, slots4, nch, 128);
     if (std::getenv("LCN_DW_ITEM")) d4.plan.item_rows = std::atoi(std::getenv("LCN_DW_ITEM"));
-    if (std::getenv("LCN_DW_SUB") && d4.plan.stride == 8) {
-      const int rounds = d4.plan.n_slots / (8 * d4.plan.sub);
-      d4.plan.sub = std::atoi(std::getenv("LCN_DW_SUB"));
-      d4.plan.n_slots = 8 * rounds * d4.plan.sub;
-    }
     const std::vector<int4> map4 = make_dw_wgmap(d4.ngroups, d4.plan, B);
     d4.wgmap = dev(map4);
     d4.n_wg = (int)map4.size();
-    std::printf("dwg plan: %d groups, items of %d rows, stride %d, %d partials per block (sub %d), %d workgroups (resident slots %d)\n",
-                d4.ngroups, d4.plan.item_rows, d4.plan.stride, d4.plan.n_slots, d4.plan.sub, d4.n_wg, slots4);
-  }
-
-  {  // the two weight-gradient kernels against each other: dW (sums in another order) and the stored dz
-    std::vector<float> w0((size_t)H * H), w1((size_t)H * H), z0((size_t)B * H), z1((size_t)B * H);
-    for (int pro = 0; pro < 2; ++pro) {
-      d.pro_scale = d4.pro_scale = pro ? sc : nullptr;
-      d.pro_shift = d4.pro_shift = pro ? sh : nullptr;
-      d.d_bnback = d4.d_bnback = 1;
-      CK(hipMemsetAsync(dW, 0, (size_t)H * H * 4, s));
-      CK(hipMemsetAsync(dzo, 0, (size_t)B * H * 4, s));
-      launch_gemm_dw(d, s);
-      launch_dw_reduce(part, dw_plan_slots(d.plan), nblk, dblk, dW, H, H, H, s);
-      CK(hipStreamSynchronize(s));
-      CK(hipMemcpy(w0.data(), dW, w0.size() * 4, hipMemcpyDeviceToHost));
-      CK(hipMemcpy(z0.data(), dzo, z0.size() * 4, hipMemcpyDeviceToHost));
-      CK(hipMemsetAsync(dW, 0, (size_t)H * H * 4, s));
-      CK(hipMemsetAsync(dzo, 0, (size_t)B * H * 4, s));
-      launch_gemm_dwg(d4, s);
-      launch_dw_reduce(part, dw_plan_slots(d4.plan), nblk, dblk, dW, H, H, H, s);
-      CK(hipStreamSynchronize(s));
-      CK(hipMemcpy(w1.data(), dW, w1.size() * 4, hipMemcpyDeviceToHost));
-      CK(hipMemcpy(z1.data(), dzo, z1.size() * 4, hipMemcpyDeviceToHost));
-      double num = 0, den = 0;
-      for (size_t i = 0; i < w0.size(); ++i) { num += (double)(w0[i] - w1[i]) * (w0[i] - w1[i]); den += (double)w0[i] * w0[i]; }
-      size_t zbad = 0;
-      for (size_t i = 0; i < z0.size(); ++i) zbad += z0[i] != z1[i];
-      std::printf("dwg vs dw (pro %d): relative difference of dW %.3g (norm %.3g), dz words that differ %zu\n", pro,
-                  std::sqrt(num / (den + 1e-300)), std::sqrt(den), zbad);
-    }
+    std::printf("dw4 plan: %d groups (%d of %d blocks), items of %d rows, stride %d, %d partials per block (sub %d), %d workgroups (resident slots %d)\n",
+                d4.ngroups, nblk4, nblk, d4.plan.item_rows, d4.plan.stride, d4.plan.n_slots, d4.plan.sub, d4.n_wg, slots4);
   }
 
   struct Case { const char* name; int kind; int pro; int variant; };
@@ -334,9 +285,9 @@ int main(int argc, char** argv) {
   cases.push_back({"dw raw", 2, PRO_RAW, 0});
   cases.push_back({"dw bnact x bnback", 2, PRO_BNACT, 0});
   cases.push_back({"dw raw x bnback", 2, PRO_BNBACK, 0});
-  cases.push_back({"dwg raw", 5, PRO_RAW, 0});
-  cases.push_back({"dwg bnact x bnback", 5, PRO_BNACT, 0});
-  cases.push_back({"dwg raw x bnback", 5, PRO_BNBACK, 0});
+  cases.push_back({"dw4 raw", 5, PRO_RAW, 0});
+  cases.push_back({"dw4 bnact x bnback", 5, PRO_BNACT, 0});
+  cases.push_back({"dw4 raw x bnback", 5, PRO_BNBACK, 0});
   if (argc > 5) {  // keep only the cases whose name contains argv[5]
     std::vector<Case> keep;
     for (const Case& c : cases)
@@ -351,8 +302,7 @@ int main(int argc, char** argv) {
           d4.pro_scale = c.pro == PRO_BNACT ? sc : nullptr;
           d4.pro_shift = c.pro == PRO_BNACT ? sh : nullptr;
           d4.d_bnback = c.pro != PRO_RAW;
-          launch_gemm_dwg(d4, s);
-          if (!std::getenv("LCN_DWG_NOREDUCE")) launch_dw_reduce(part, dw_plan_slots(d4.plan), nblk, dblk, dW, H, H, H, s);
+          launch_gemm_dw4(d4, s);  // (no reduce: the kernel alone)
         } else if (c.kind == 2) {
           d.pro_scale = c.pro == PRO_BNACT ? sc : nullptr;
           d.pro_shift = c.pro == PRO_BNACT ? sh : nullptr;

@@ -1,52 +1,55 @@
-// Weight-gradient GEMM, up to FOUR blocks of one output slab per workgroup
-// (gfx950).
+// Weight-gradient GEMM, FOUR blocks of one output slab per workgroup (gfx950).
 //
 // Same contract as gemm_dw_kernel (kernels_gemm.hip): dW_e(si, so) = A[:, si]^T .
 // dZ[:, so] over a workgroup's items of the batch, one partial slab per block
-// and slot.  Here a group is 1..4 blocks (si_0.., so) -- dwg_body has the two
-// wave-to-tile maps -- and the staged D slab -- its two loads per thread, its BN-backward rebuild,
-// its transposed scatter -- serves up to four blocks instead of two: a 32-row
-// stage holds up to 64 MFMAs per wave between its two barriers, and an output
-// slab's dh / z rows are read by about half as many workgroups.  <= 168 VGPRs,
-// 49 KB of LDS: three workgroups per CU.
+// and slot.  Here a group is four blocks (si_0..si_3, so) and wave w owns block
+// w whole (64 x 64: four 32x32 accumulators), so the staged D slab -- its two
+// loads per thread, its BN-backward rebuild, its transposed scatter -- serves
+// four blocks instead of two, a 32-row stage holds 64 MFMAs per wave between
+// its two barriers instead of 32 (four fragment reads per 16 MFMAs), and an
+// output slab's dh / z rows are read by half as many workgroups.  146-168
+// VGPRs, 49 KB of LDS: three workgroups per CU.
 //
-// Measured in gemm_bench only (B = 65 536, knn 3, one box per comparison; raw /
-// BN-backward D / + BN-apply A, % of the fp32 MFMA peak, kernel alone):
-//   * the 37 complete quads (148 of 175 blocks), a whole block per wave:
-//     80.6 / 77.3 / 73.0 % against 80.0 / 72.5 / 68.7 % for the two-block kernel
-//     over all blocks; with the sub-tile map instead 76.3 / 73.4 / 71.8 %;
-//   * all 175 blocks in one launch (fours, then the remainder of an output slab
-//     as one group of 1..3: 37 + 17 groups): 774 / 845 / 1139 us against 753 /
-//     853 / 885 us -- the remainders (the output slabs hold 5..17 blocks) run
-//     slower at three workgroups per CU than they do now at four, and the
-//     BN-apply x BN-backward instance spills (27 registers) beside its 64
-//     accumulator and 48 staging registers.
-// Not part of liblcn.
+// Runs the hidden layers where every output slab holds a multiple of four
+// blocks (four slabs per joint: the cfg4 shape, 68 blocks a slab; 16 384 rows:
+// 5.34-5.48 -> 5.20 ms a launch, the step 180.2-184.2 -> 177.9-178.0 ms on one
+// box).  Measured in gemm_bench at cfg3 (B = 65 536, knn 3; raw / BN-backward D /
+// + BN-apply A, % of the fp32 MFMA peak): the 37 complete quads (148 of 175
+// blocks) 78.2 / 74.2 / 71.6 % for the kernel alone against 79.3 / 71.3 / 68.5 %
+// for the two-block kernel over all blocks with its partial reduce (2 %).  With
+// one slab per joint the output slabs hold 5..17 blocks, and no way of running
+// the 27 blocks left over (a launch of their own; a sub-tile wave map for groups
+// of 1..3 in the same launch at three workgroups per CU; a sub-tile map for every
+// group size) kept more than 2 % of that over all blocks, so there the two-block
+// kernel stays.
 #include "gemm_common.h"
 
 namespace lcn {
 
 constexpr int kDw4Ld = 36;
 
-// The whole workgroup for one group shape.  QUAD (four blocks): wave w owns
-// block w whole, four accumulators = (rows 0..31 | 32..63) x (columns 0..31 |
-// 32..63), four fragment reads per 16 MFMAs.  Otherwise (1..3 blocks): wave
-// (ph, qh) owns the 32 x 32 sub-tile (rows 32ph.., columns 32qh..) of every block
-// of the group, one accumulator a block, so no wave idles.
-template <bool PRO, bool DBB, bool DROP, bool QUAD>
-__device__ __forceinline__ void dwg_body(const GemmDwArgs& a, float* Ds, float (*As)[64 * kDw4Ld], float* tab, int gi,
-                                         int slot, int item0, int n_it, const int4 grp, const int4 gb) {
+template <bool PRO, bool DBB, bool DROP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void gemm_dw4_kernel(GemmDwArgs a) {
+  __shared__ __attribute__((aligned(16))) float Ds[64 * kDw4Ld];      // [q][row]
+  __shared__ __attribute__((aligned(16))) float As[4][64 * kDw4Ld];   // [p][row] per block
+  // channel constants: A (sc, sh) of the four input slabs; D sc, sh, c1, c2, c3, c1 * alpha
+  __shared__ __attribute__((aligned(16))) float tab[14 * 64];
+  const int4 wgm = a.wgmap[blockIdx.x];
+  const int gi = __builtin_amdgcn_readfirstlane(wgm.x), slot = __builtin_amdgcn_readfirstlane(wgm.y);
+  const int item0 = __builtin_amdgcn_readfirstlane(wgm.z), n_it = __builtin_amdgcn_readfirstlane(wgm.w);
+  if (gi < 0) return;  // padding of the grid (uniform per workgroup)
+  // group: (so, 4, rank, count), (b0, b1, b2, b3)
+  const int4 grp = a.groups[2 * gi], gb = a.groups[2 * gi + 1];
   const DwPlan pl = a.plan;
   const int so = __builtin_amdgcn_readfirstlane(grp.x);
-  const int nb = QUAD ? 4 : __builtin_amdgcn_readfirstlane(grp.y);
   const int bq[4] = {__builtin_amdgcn_readfirstlane(gb.x), __builtin_amdgcn_readfirstlane(gb.y),
                      __builtin_amdgcn_readfirstlane(gb.z), __builtin_amdgcn_readfirstlane(gb.w)};
   int si[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) si[k] = __builtin_amdgcn_readfirstlane(a.blk[bq[k] >= 0 ? bq[k] : bq[0]].x);
+  for (int k = 0; k < 4; ++k) si[k] = __builtin_amdgcn_readfirstlane(a.blk[bq[k]].x);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wv = __builtin_amdgcn_readfirstlane(w);
-  const int lr = lane & 31, h = lane >> 5, ph = wv >> 1, qh = wv & 1;
+  const int lr = lane & 31, h = lane >> 5;
   const int wrank = __builtin_amdgcn_readfirstlane(grp.z), wcount = __builtin_amdgcn_readfirstlane(grp.w);
   const bool may_write = DBB && a.dz_out != nullptr;
   const int R = pl.item_rows, istride = pl.stride;
@@ -67,7 +70,7 @@ __device__ __forceinline__ void dwg_body(const GemmDwArgs& a, float* Ds, float (
     }
   }
 
-  f32x16 acc0, acc1, acc2, acc3;  // this wave's sub-tile of blocks 0..3
+  f32x16 acc0, acc1, acc2, acc3;  // this wave's block: (rows 0..31 | 32..63) x (columns 0..31 | 32..63)
 #pragma unroll
   for (int k = 0; k < 16; ++k) { acc0[k] = 0.f; acc1[k] = 0.f; acc2[k] = 0.f; acc3[k] = 0.f; }
   [[maybe_unused]] Dropout dr{};
@@ -99,7 +102,7 @@ __device__ __forceinline__ void dwg_body(const GemmDwArgs& a, float* Ds, float (
     const int t_ = (BASE) / kRT;                                           \
     const int od = (int)((unsigned)(t_ * S_d + so) * 8192u);               \
     _Pragma("unroll") for (int k = 0; k < 4; ++k) {                        \
-      if (k < nb) {                                                 \
+      {                                                                    \
         const int oa = (int)((unsigned)(t_ * S_a + si[k]) * 8192u);        \
         ra[k][0] = DW_BUFLD(ares, v40, oa);                                \
         ra[k][1] = DW_BUFLD(ares, v41, oa);                                \
@@ -128,17 +131,16 @@ __device__ __forceinline__ void dwg_body(const GemmDwArgs& a, float* Ds, float (
     const bool writer = may_write && item % wcount == wrank;
     __syncthreads();  // previous stage's fragment reads are done (and the tables written)
     const bool v0 = base + sr < r1, v1 = base + sr + 16 < r1;
-    if constexpr (PRO) {
-      const float ba = (1.f - a.alpha) / (1.f + a.alpha);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (k < nb) {
-          const float4 sc = *(const float4*)(tab + 128 * k + f0), sh = *(const float4*)(tab + 128 * k + 64 + f0);
-          ra[k][0] = bnact4_scaled(ra[k][0], sc, sh, ba);
-          ra[k][1] = bnact4_scaled(ra[k][1], sc, sh, ba);
-        }
-      }
-    }
+    // transposed scatter: feature -> LDS row, batch row -> column
+#define DW_PUT(P, F4, OFF)             \
+  P[(OFF)] = (F4).x;                   \
+  P[(OFF) + kDw4Ld] = (F4).y;          \
+  P[(OFF) + 2 * kDw4Ld] = (F4).z;      \
+  P[(OFF) + 3 * kDw4Ld] = (F4).w;
+    const int o0 = f0 * kDw4Ld + sr, o1 = o0 + 16;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);  // rows past the item's end contribute nothing
+    // the D slab first (its coefficients are dead before the A slabs' tables are read), then block by
+    // block: no instance spills (all four blocks transformed ahead of the scatter: 28 registers spilled)
     if constexpr (DBB) {
       BnBackCoef cf;
       cf.sc = *(const float4*)(tab + 512 + f0); cf.sh = *(const float4*)(tab + 576 + f0);
@@ -166,32 +168,28 @@ __device__ __forceinline__ void dwg_body(const GemmDwArgs& a, float* Ds, float (
         if (v1) o[(t_ * S_d + so) * 512 + c41] = rd1;
       }
     }
-    {  // rows past the item's end contribute nothing
-      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!v0) { ra[0][0] = z4; ra[1][0] = z4; ra[2][0] = z4; ra[3][0] = z4; rd0 = z4; }
-      if (!v1) { ra[0][1] = z4; ra[1][1] = z4; ra[2][1] = z4; ra[3][1] = z4; rd1 = z4; }
-    }
-    {
-      // transposed scatter: feature -> LDS row, batch row -> column
-#define DW_PUT(P, F4, OFF)             \
-  P[(OFF)] = (F4).x;                   \
-  P[(OFF) + kDw4Ld] = (F4).y;          \
-  P[(OFF) + 2 * kDw4Ld] = (F4).z;      \
-  P[(OFF) + 3 * kDw4Ld] = (F4).w;
-      const int o0 = f0 * kDw4Ld + sr, o1 = o0 + 16;
+    if (!v0) rd0 = z4;
+    if (!v1) rd1 = z4;
+    DW_PUT(Ds, rd0, o0) DW_PUT(Ds, rd1, o1)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (k < nb) { DW_PUT(As[k], ra[k][0], o0) DW_PUT(As[k], ra[k][1], o1) }
+    for (int k = 0; k < 4; ++k) {
+      if constexpr (PRO) {
+        const float ba = (1.f - a.alpha) / (1.f + a.alpha);
+        const float4 sc = *(const float4*)(tab + 128 * k + f0), sh = *(const float4*)(tab + 128 * k + 64 + f0);
+        ra[k][0] = bnact4_scaled(ra[k][0], sc, sh, ba);
+        ra[k][1] = bnact4_scaled(ra[k][1], sc, sh, ba);
       }
-      DW_PUT(Ds, rd0, o0) DW_PUT(Ds, rd1, o1)
-#undef DW_PUT
+      if (!v0) ra[k][0] = z4;
+      if (!v1) ra[k][1] = z4;
+      DW_PUT(As[k], ra[k][0], o0) DW_PUT(As[k], ra[k][1], o1)
     }
+#undef DW_PUT
     // the next stage's loads go out before the barrier (its wait hides part of
     // their latency), and the MFMA phase runs at raised wave priority
     if (nmore) DW_GLOAD(nbase);
     __syncthreads();
     __builtin_amdgcn_s_setprio(1);
-    if constexpr (QUAD) {
+    {
       const float* A0 = As[wv] + lr * kDw4Ld + 4 * h;
       const float* A1 = As[wv] + (32 + lr) * kDw4Ld + 4 * h;
       const float* D0 = Ds + lr * kDw4Ld + 4 * h;
@@ -200,28 +198,11 @@ __device__ __forceinline__ void dwg_body(const GemmDwArgs& a, float* Ds, float (
       for (int g = 0; g < 4; ++g) {
         const float4 a0 = *(const float4*)(A0 + 8 * g), a1 = *(const float4*)(A1 + 8 * g);
         const float4 d0 = *(const float4*)(D0 + 8 * g), d1 = *(const float4*)(D1 + 8 * g);
-#define DWG_Q(C)                                                                \
+#define DW4_K(C)                                                                \
         acc0 = MFMA32(a0.C, d0.C, acc0); acc1 = MFMA32(a0.C, d1.C, acc1);       \
         acc2 = MFMA32(a1.C, d0.C, acc2); acc3 = MFMA32(a1.C, d1.C, acc3);
-        DWG_Q(x) DWG_Q(y) DWG_Q(z) DWG_Q(w)
-#undef DWG_Q
-      }
-    } else {
-      const float* Dq = Ds + (32 * qh + lr) * kDw4Ld + 4 * h;
-      const float* Ap = &As[0][0] + (32 * ph + lr) * kDw4Ld + 4 * h;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 dv = *(const float4*)(Dq + 8 * g);
-        const float4 a0 = *(const float4*)(Ap + 8 * g);
-        float4 a1 = a0, a2 = a0;
-        if (nb > 1) a1 = *(const float4*)(Ap + 64 * kDw4Ld + 8 * g);
-        if (nb > 2) a2 = *(const float4*)(Ap + 2 * 64 * kDw4Ld + 8 * g);
-#define DWG_K(C)                                       \
-        acc0 = MFMA32(a0.C, dv.C, acc0);               \
-        if (nb > 1) acc1 = MFMA32(a1.C, dv.C, acc1);   \
-        if (nb > 2) acc2 = MFMA32(a2.C, dv.C, acc2);
-        DWG_K(x) DWG_K(y) DWG_K(z) DWG_K(w)
-#undef DWG_K
+        DW4_K(x) DW4_K(y) DW4_K(z) DW4_K(w)
+#undef DW4_K
       }
     }
     __builtin_amdgcn_s_setprio(0);
@@ -233,7 +214,7 @@ __device__ __forceinline__ void dwg_body(const GemmDwArgs& a, float* Ds, float (
   }
 #undef DW_GLOAD
 #undef DW_BUFLD
-  if constexpr (QUAD) {  // this slot's partial of this wave's block
+  {  // this slot's partial of this wave's block
     const int myblk = wv == 0 ? bq[0] : wv == 1 ? bq[1] : wv == 2 ? bq[2] : bq[3];
     float* out = a.part + ((size_t)slot * a.nblk + myblk) * 4096;
 #pragma unroll
@@ -244,63 +225,34 @@ __device__ __forceinline__ void dwg_body(const GemmDwArgs& a, float* Ds, float (
       out[(32 + p) * 64 + lr] = acc2[k];
       out[(32 + p) * 64 + 32 + lr] = acc3[k];
     }
-  } else {  // this slot's partial of every block: this wave's sub-tile
-#define DWG_OUT(K, ACC)                                                        \
-  if (nb > (K)) {                                                              \
-    float* out = a.part + ((size_t)slot * a.nblk + bq[K]) * 4096 + 32 * qh;    \
-    _Pragma("unroll") for (int k = 0; k < 16; ++k) {                           \
-      const int p = 32 * ph + (k & 3) + 8 * (k >> 2) + 4 * h;                  \
-      out[p * 64 + lr] = ACC[k];                                               \
-    }                                                                          \
-  }
-    DWG_OUT(0, acc0) DWG_OUT(1, acc1) DWG_OUT(2, acc2)
-#undef DWG_OUT
   }
 }
 
-template <bool PRO, bool DBB, bool DROP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void gemm_dwg_kernel(GemmDwArgs a) {
-  __shared__ __attribute__((aligned(16))) float Ds[64 * kDw4Ld];      // [q][row]
-  __shared__ __attribute__((aligned(16))) float As[4][64 * kDw4Ld];   // [p][row] per block
-  // channel constants: A (sc, sh) of the four input slabs; D sc, sh, c1, c2, c3, c1 * alpha
-  __shared__ __attribute__((aligned(16))) float tab[14 * 64];
-  const int4 wgm = a.wgmap[blockIdx.x];
-  const int gi = __builtin_amdgcn_readfirstlane(wgm.x), slot = __builtin_amdgcn_readfirstlane(wgm.y);
-  const int item0 = __builtin_amdgcn_readfirstlane(wgm.z), n_it = __builtin_amdgcn_readfirstlane(wgm.w);
-  if (gi < 0) return;  // padding of the grid (uniform per workgroup)
-  // group: (so, blocks, rank, count), (b0, b1, b2, b3) with -1 past the group's blocks
-  const int4 grp = a.groups[2 * gi], gb = a.groups[2 * gi + 1];
-  if (__builtin_amdgcn_readfirstlane(grp.y) == 4)
-    dwg_body<PRO, DBB, DROP, true>(a, Ds, As, tab, gi, slot, item0, n_it, grp, gb);
-  else
-    dwg_body<PRO, DBB, DROP, false>(a, Ds, As, tab, gi, slot, item0, n_it, grp, gb);
-}
-
-int gemm_dwg_resident_slots() {
+int gemm_dw4_resident_slots() {
   int dev = 0, per_cu = 0;
   hipDeviceProp_t prop;
   if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm_dwg_kernel<true, true, false>, 256, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm_dw4_kernel<true, true, false>, 256, 0) != hipSuccess)
     return 0;
   return per_cu * prop.multiProcessorCount;
 }
 
-void launch_gemm_dwg(const GemmDwArgs& a, hipStream_t s) {
+void launch_gemm_dw4(const GemmDwArgs& a, hipStream_t s) {
   const int grid = a.n_wg;
   const bool pro = a.pro_scale != nullptr, dbb = a.d_bnback != 0;
   const bool drop = dbb && a.d_drop.rate > 0.f;
   if (pro && drop)
-    hipLaunchKernelGGL((gemm_dwg_kernel<true, true, true>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw4_kernel<true, true, true>), dim3(grid), dim3(256), 0, s, a);
   else if (drop)
-    hipLaunchKernelGGL((gemm_dwg_kernel<false, true, true>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw4_kernel<false, true, true>), dim3(grid), dim3(256), 0, s, a);
   else if (pro && dbb)
-    hipLaunchKernelGGL((gemm_dwg_kernel<true, true, false>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw4_kernel<true, true, false>), dim3(grid), dim3(256), 0, s, a);
   else if (pro)
-    hipLaunchKernelGGL((gemm_dwg_kernel<true, false, false>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw4_kernel<true, false, false>), dim3(grid), dim3(256), 0, s, a);
   else if (dbb)
-    hipLaunchKernelGGL((gemm_dwg_kernel<false, true, false>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw4_kernel<false, true, false>), dim3(grid), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((gemm_dwg_kernel<false, false, false>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_dw4_kernel<false, false, false>), dim3(grid), dim3(256), 0, s, a);
 }
 
 }  // namespace lcn

@@ -107,9 +107,11 @@ struct Handle {
   struct DwMap { int64_t B; DwPlan plan; int4* dev; int n; };   // workgroup map of a launch (make_dw_wgmap)
   struct DwGroups {
     int4* dev = nullptr; int n = 0;
+    bool quad = false;           // groups of four blocks, two int4 a group (gemm_dw4.hip)
+    int slots = 0;               // quad: workgroups of that kernel the GPU holds at once
     std::vector<DwMap> maps;     // made on first use per batch size
   };
-  DwGroups grp_hidden, grp_lift, grp_out;
+  DwGroups grp_hidden, grp_lift, grp_out;   // grp_hidden.quad: groups of four blocks (gemm_dw4.hip)
   int dw_slots = 0;               // weight-gradient workgroups the GPU holds at once
 
   std::vector<BnStats> bn;
@@ -243,10 +245,34 @@ int gemm_pair_mode();
 // (so, block0, block1 | -1, rank | count << 8): the group's rank among the
 // groups of its output slab and their number -- they all rebuild the same dz
 // and take turns storing it (item i is stored by the group of rank i % count).
-int upload_dw_groups(Handle* h, const std::vector<int2>& blk, Handle::DwGroups* out) {
+int upload_dw_groups(Handle* h, const std::vector<int2>& blk, Handle::DwGroups* out, bool try_quads = false) {
   int nso = 0;
   for (const int2& b : blk) nso = std::max(nso, b.y + 1);
   std::vector<int4> g;
+  // Four blocks a group where every output slab holds a multiple of four (several
+  // slabs per joint; the cfg4 shape: 68): the kernel that shares the staged dz
+  // between four blocks (cfg4 shape, 16 384 rows: 5.23 -> 4.98 ms a launch).  Two int4 per
+  // group: (so, 4, rank, count), (b0, b1, b2, b3).  LCN_DW_QUAD=0: never.
+  bool quads = try_quads && !(std::getenv("LCN_DW_QUAD") && std::atoi(std::getenv("LCN_DW_QUAD")) == 0) &&
+               blk.size() < 65536;
+  std::vector<std::vector<int>> by_so(nso);
+  for (size_t b = 0; b < blk.size(); ++b) by_so[blk[b].y].push_back((int)b);
+  for (const auto& ids : by_so) quads = quads && !ids.empty() && ids.size() % 4 == 0;
+  if (quads) {
+    for (int so = 0; so < nso; ++so) {
+      const auto& ids = by_so[so];
+      const int count = (int)ids.size() / 4;
+      for (int q = 0; q < count; ++q) {
+        g.push_back(make_int4(so, 4, q, count));
+        g.push_back(make_int4(ids[4 * q], ids[4 * q + 1], ids[4 * q + 2], ids[4 * q + 3]));
+      }
+    }
+    out->n = (int)g.size() / 2;
+    out->quad = true;
+    out->slots = gemm_dw4_resident_slots();
+    if (out->slots <= 0) { h->err = "occupancy query of the weight-gradient kernel failed"; return LCN_E_HIP; }
+    return upload(h, &out->dev, g);
+  }
   for (int so = 0; so < nso; ++so) {
     std::vector<int> ids;
     for (size_t b = 0; b < blk.size(); ++b)
@@ -280,7 +306,7 @@ int dw_chunks(int nblk, int64_t B) {
 // contiguous chunks).
 DwPlan dw_plan(const Handle* h, const Handle::DwGroups& g, int nblk, int64_t B) {
   static const int slots_env = std::getenv("LCN_DW_SLOTS") ? std::atoi(std::getenv("LCN_DW_SLOTS")) : -1;
-  return make_dw_plan(B, g.n, slots_env >= 0 ? slots_env : h->dw_slots, dw_chunks(nblk, B), 128);
+  return make_dw_plan(B, g.n, slots_env >= 0 ? slots_env : (g.slots > 0 ? g.slots : h->dw_slots), dw_chunks(nblk, B), 128);
 }
 
 // Launches of at most this many 32-row tiles run the small-batch kernel, which
@@ -391,7 +417,7 @@ int build(Handle* h, const lcn_config* c) {
     bptr.push_back((int)bidx.size());
   }
   CHECK(upload(h, &h->blk, blk));
-  CHECK(upload_dw_groups(h, blk, &h->grp_hidden));
+  CHECK(upload_dw_groups(h, blk, &h->grp_hidden, true));
   CHECK(upload(h, &h->fwd_ptr, fptr));
   CHECK(upload(h, &h->bwd_ptr, bptr));
   CHECK(upload(h, &h->fwd_idx, fidx));
@@ -953,7 +979,8 @@ int gemm_dw(Handle* h, const Operand& A, const Operand& D, const int2* blk, int 
   a.part = h->dw_part;
   hipEvent_t ev[2];
   if (timer >= 0) tstart(h, timer, ev);
-  launch_gemm_dw(a, h->stream);
+  if (g->quad) launch_gemm_dw4(a, h->stream);
+  else launch_gemm_dw(a, h->stream);
   if (timer >= 0)
     tstop(h, timer, ev, timer == LCN_K_GEMM_DW ? 2.0 * 4096.0 * nblk * B : 4.0 * (h->H + 51) * (double)B);
   launch_dw_reduce(h->dw_part, dw_plan_slots(a.plan), nblk, blk, dW, ld, rows_valid, cols_valid, h->stream);

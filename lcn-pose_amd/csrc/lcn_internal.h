@@ -361,17 +361,10 @@ struct GemmDwArgs {
 void launch_gemm_dw(const GemmDwArgs& a, hipStream_t s);
 // workgroups of the weight-gradient kernel the current device holds at once
 int gemm_dw_resident_slots();
-// up to four blocks of an output slab per workgroup (gemm_dwg.hip): two int4
-// per group, (so, blocks, rank, count) and (b0, b1, b2, b3) with -1 past the
-// group's blocks
-void launch_gemm_dwg(const GemmDwArgs& a, hipStream_t s);
-int gemm_dwg_resident_slots();
-// the groups of an output slab that holds d blocks: fours, then the rest (1..3) as one group
-inline std::vector<int> dwg_group_sizes(int d) {
-  std::vector<int> g(d / 4, 4);
-  if (d % 4) g.push_back(d % 4);
-  return g;
-}
+// four blocks of an output slab per workgroup (gemm_dw4.hip): two int4 per
+// group, (so, 4, rank, count) and (b0, b1, b2, b3)
+void launch_gemm_dw4(const GemmDwArgs& a, hipStream_t s);
+int gemm_dw4_resident_slots();
 // sum partials over chunks; write into dense dW [rows][ld] at (si*64+p, so*64+q),
 // dropping rows >= rows_valid / columns >= cols_valid (padding of thin layers)
 void launch_dw_reduce(const float* part, int nchunks, int nblk, const int2* blk,

@@ -20,6 +20,9 @@ CASES = [
     ("lc_knn2_L3", dict(F=64, L=3, knn=2), 300),
     ("lc_knn5_L1", dict(F=64, L=1, knn=5), 64),
     ("exp_L2_F128", dict(F=128, L=2, knn=2, mask="exponential"), 96),
+    # four slabs per joint, every joint pair: 68 blocks an output slab, the weight
+    # gradient in groups of four blocks (gemm_dw4.hip)
+    ("exp_L1_F256", dict(F=256, L=1, knn=2, mask="exponential"), 64),
     # three slabs per joint: two pair up, the third finds its partner across joints
     ("lc_F192_knn4", dict(F=192, L=1, knn=4), 70),
     ("lc_inF3", dict(F=64, L=1, knn=3, in_F=3), 160),
@@ -94,6 +97,14 @@ def test_gradients_match_oracle(name, kw, B, gemm_path):
     assert not bad, f"relative gradient errors above 1e-4: {bad}"
     # params unchanged without update
     np.testing.assert_array_equal(net.get_params(), O.flatten(cfg, params))
+
+
+def test_weight_gradient_in_pairs_of_blocks_at_four_slabs_per_joint(monkeypatch):
+    """LCN_DW_QUAD=0 keeps the two-block weight-gradient kernel where the
+    four-block one would run (every output slab a multiple of four blocks):
+    the same gradients."""
+    monkeypatch.setenv("LCN_DW_QUAD", "0")
+    test_gradients_match_oracle("exp_L1_F256", dict(F=256, L=1, knn=2, mask="exponential"), 64, "default")
 
 
 def test_adam_step_matches_oracle(gemm_path):
