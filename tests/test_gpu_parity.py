@@ -152,6 +152,36 @@ def test_duplicated_batch_gives_same_gradients():
         assert rel_err(g2[off:off + n], g1[off:off + n]) < 1e-4, name
 
 
+@pytest.mark.parametrize("kw,B", [(dict(F=64, L=2, knn=3), 8192 + 40),
+                                  (dict(F=256, L=1, knn=2, mask="exponential"), 2624)],
+                         ids=["lc_F64", "exp_F256"])
+def test_training_steps_are_bitwise_reproducible(kw, B):
+    """The same three training steps on two handles: losses, gradients and the
+    updated parameters agree bit for bit.  Nothing in a step depends on the
+    order in which workgroups finish: the batch statistics are summed in a
+    fixed order (the workgroup that finishes the column sums last only runs
+    the per-channel finish), every weight-gradient partial has one writer and
+    the partials are added in slot order, the stored dz has one writer per
+    item.  Batches of the large-batch kernels (one and two output slabs per
+    workgroup, two and four blocks per weight-gradient workgroup)."""
+    cfg = make_cfg(**kw)
+    params = O.flatten(cfg, perturbed_params(cfg))
+    runs = []
+    for _ in range(2):
+        net = make_network(cfg, max_batch=B)
+        net.set_params(params)
+        losses, grads = [], None
+        for step in range(3):
+            x, lab = synthetic_batch(B, cfg.in_F, seed=20 + step)
+            loss, _ = net.train_step(x, lab, keep_grads=True)
+            losses.append(loss)
+            grads = net.get_grads().copy()
+        runs.append((np.array(losses), grads, net.get_params().copy()))
+        net.close()
+    for a, b in zip(runs[0], runs[1]):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_duplicated_batch_gives_same_gradients_cfg4_shape():
     """The same property at BASELINE.json configs[3]'s model shape (dense
     exponential mask, F 256, 6 blocks, H 4352) and its per-GPU batch on 8
