@@ -392,6 +392,17 @@ def read_timers(net, steps):
     return kern, bn_act_timing, thin_timing
 
 
+def collective_timing(net, steps):
+    """The all-reduces of the timed steps on this rank (HIP events around each
+    on the compute stream: enqueue to completion, so with the wait for the
+    slowest rank), or None on a handle that is not joined."""
+    n, ms, nbytes = net.kernel_timing(native.K_COMM)
+    if not n:
+        return None
+    return {"per_step": n / steps, "ms_per_step": round(ms / steps, 4), "avg_us": round(1e3 * ms / n, 2),
+            "bytes_per_step": int(nbytes / steps)}
+
+
 def pmc_traffic(args, B, kernel):
     """HBM bytes per launch of `kernel` from the committed PMC passes -- they
     were collected on the cfg3 model shape at 65 536 rows and apply only there."""
@@ -548,6 +559,7 @@ def main(argv=None):
     elapsed = time.perf_counter() - t0
     elapsed = float(net.allreduce_host([elapsed], op="max")[0])
     kern, bn_act_timing, thin_timing = read_timers(net, args.steps)
+    comm_timing = collective_timing(net, args.steps)
     net.set_timing(False)
 
     # forward-only rate (BASELINE configs[1], cfg2: `--config cfg2` gives it a
@@ -592,6 +604,7 @@ def main(argv=None):
                        + (", one-rank RCCL communicator" if world == 1 and args.rccl_self else "")},
             **roofline_blocks(args, B, kern, bn_act_timing, thin_timing), **comm_fields(net),
             "collectives_per_step": (4 * args.layers + 3) if (world > 1 or args.rccl_self) else 0,
+            "collectives": comm_timing,
             "fwd_only_poses_per_s": round(G * nf / tfwd, 1),
             "host_input_poses_per_s": round(G * nh / thost, 1),
         }

@@ -252,9 +252,12 @@ uint32_t lcn_crc32c(uint32_t crc, const void* data, int64_t n);
  * the block outputs; LCN_K_LIFT / LCN_K_OUT / LCN_K_OUT_DW: the thin lift
  * (models_att.py:729) and output (:765) layers' forward launches and the
  * output layer's weight gradient.  For these HBM-bound kernels the "flops"
- * field accumulates algorithmic HBM bytes (inputs read + outputs written). */
+ * field accumulates algorithmic HBM bytes (inputs read + outputs written).
+ * LCN_K_COMM: the all-reduces of a step on a joined handle (RCCL or the host
+ * exchange), from enqueue to completion on the compute stream -- so with the
+ * wait for the slowest rank; "flops" accumulates the bytes reduced. */
 enum { LCN_K_GEMM_FWD = 0, LCN_K_GEMM_DX = 1, LCN_K_GEMM_DW = 2, LCN_K_BN_ACT = 3, LCN_K_LIFT = 4,
-       LCN_K_OUT = 5, LCN_K_OUT_DW = 6, LCN_K_NUM = 7 };
+       LCN_K_OUT = 5, LCN_K_OUT_DW = 6, LCN_K_COMM = 7, LCN_K_NUM = 8 };
 /* enable: 0 = off, 1 = HIP-event timers around every kernel class above, or a
  * set of bits 1 << (1 + LCN_K_x) to time only those classes (timing-only
  * events: two records per timed launch, no system fence).  Resets the accumulated timings. */

@@ -629,13 +629,26 @@ bool multi(const Handle* h) { return has_comm(h) && !h->comm_off; }
 
 // In-place all-reduce of a device buffer over the ranks, stream-ordered: RCCL,
 // or (host exchange) device -> host, the caller's function, host -> device.
+void tstart(Handle* h, int k, hipEvent_t* pair);
+void tstop(Handle* h, int k, hipEvent_t* pair, double flops);
+
+int allreduce_untimed(Handle* h, void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op);
+
 int allreduce(Handle* h, void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op = ncclSum) {
   if (h->comm_off) return LCN_OK;  // suspended: the call runs rank-locally (phased reductions included)
+  if (!h->comm && !h->host_ar) return LCN_OK;
+  hipEvent_t ev[2];
+  tstart(h, LCN_K_COMM, ev);
+  const int rc = allreduce_untimed(h, buf, count, dt, op);
+  tstop(h, LCN_K_COMM, ev, (double)count * (dt == ncclDouble ? 8 : 4));
+  return rc;
+}
+
+int allreduce_untimed(Handle* h, void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op) {
   if (h->comm) {
     NCCLC(ncclAllReduce(buf, buf, count, dt, op, h->comm, h->stream));
     return LCN_OK;
   }
-  if (!h->host_ar) return LCN_OK;
   const size_t bytes = count * (dt == ncclDouble ? 8 : 4);
   if (h->host_stage.size() < bytes) h->host_stage.resize(bytes);
   HIPC(hipMemcpyAsync(h->host_stage.data(), buf, bytes, hipMemcpyDeviceToHost, h->stream));

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("LCN_LIB", os.path.join(HERE, "liblcn.so"))
 LCN_ABI_VERSION = 2
 MASK_LOCALLY_CONNECTED, MASK_EXPONENTIAL = 0, 1
 IN_DEVICE, OUT_DEVICE, NO_UPDATE, KEEP_GRADS, ASYNC = 1, 2, 4, 8, 16
-K_GEMM_FWD, K_GEMM_DX, K_GEMM_DW, K_BN_ACT, K_LIFT, K_OUT, K_OUT_DW = 0, 1, 2, 3, 4, 5, 6
+K_GEMM_FWD, K_GEMM_DX, K_GEMM_DW, K_BN_ACT, K_LIFT, K_OUT, K_OUT_DW, K_COMM = 0, 1, 2, 3, 4, 5, 6, 7
 DTYPE_F32, DTYPE_F64 = 0, 1
 MAX_DATASETS, MAX_COPIES = 16, 8
 AUG_NONE, AUG_FLIP, AUG_ROTATE, AUG_TRANSLATE = 0, 1, 2, 3

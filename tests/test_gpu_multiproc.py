@@ -44,6 +44,10 @@ def test_bench_gpus_2_runs_two_ranks_and_reports_them():
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["value"] > 0
     assert d["config"]["global_batch"] == 4096 and d["config"]["per_gpu_batch"] == 2048
     assert d["cpu_baseline"] is None and d["roofline"]["frac"] > 0
+    # the exchanges of a step as rank 0 timed them: 4 L + 3 all-reduces, the gradient vector among them
+    assert d["comm"] == "host" and d["collectives_per_step"] == 15
+    c = d["collectives"]
+    assert c["per_step"] == 15 and c["ms_per_step"] > 0 and c["bytes_per_step"] > 4 * 7_000_000
 
 
 def test_bench_fails_when_a_rank_fails():
